@@ -1,0 +1,676 @@
+// hcrag_index.hip — host side of the node-embedding index C ABI (include/hcrag.h).
+//
+// Replaces, for HC-RAG's vector path:
+//   experiments/main.py:762       embeddings_matrix = np.array(pickled embeddings)   -> hcr_index_add
+//   experiments/main.py:841-849   cosine_similarity + argsort[::-1][:k] + threshold  -> hcr_search
+//   experiments/main.py:872-889   category filter + the same search                 -> rowmask
+//   experiments/isRelevant.py:197-210  batch_semantic_similarity (all scores)        -> hcr_score_all
+//   llama-index SimpleVectorStore.query / get_top_k_embeddings (query_interface.py:200-204)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "hcrag.h"
+#include "topk_kernels.h"
+
+using namespace hcr;
+
+// ---------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPC(expr)                                                                       \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      return set_err(e_ == hipErrorOutOfMemory ? HCR_ENOMEM : HCR_EHIP, "%s: %s (%s:%d)", \
+                     #expr, hipGetErrorString(e_), __FILE__, __LINE__);                  \
+    }                                                                                    \
+  } while (0)
+
+#define CHECK(expr)              \
+  do {                           \
+    int rc_ = (expr);            \
+    if (rc_ != HCR_OK) return rc_; \
+  } while (0)
+
+extern "C" const char* hcr_last_error(void) { return g_err.c_str(); }
+extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.1.0 (gfx950)"; }
+extern "C" int hcr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---------------------------------------------------------------------------------------
+// index object
+// ---------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (want <= bytes) return HCR_OK;
+    if (p) { HIPC(hipFree(p)); p = nullptr; bytes = 0; }
+    want = std::max<size_t>(want, 256);
+    HIPC(hipMalloc(&p, want));
+    bytes = want;
+    return HCR_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct hcr_index {
+  int device = 0;
+  int dim = 0;
+  int ld = 0;           // row stride in elements (dim rounded up to 64, zero padded)
+  int dtype = HCR_F16;  // storage dtype
+  int64_t n = 0;
+  int64_t cap = 0;      // allocated rows (multiple of 128)
+  int64_t id_offset = 0;
+  DevBuf rows, norm64, inv32, maskbits, rho;
+  bool has_mask = false;
+  bool rho_dirty = true;
+  double rho_host = 0.0;
+  hipStream_t stream = nullptr;
+  // search workspace
+  DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
+      w_unc, w_cnt;
+  hcr_search_stats stats{};
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static size_t dtype_size(int dt) { return dt == HCR_F32 ? 4 : 2; }
+static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows);
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+extern "C" int hcr_index_create(int device, int dim, int dtype, int64_t capacity_rows,
+                                hcr_index** out) {
+  if (!out) return set_err(HCR_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (dim <= 0 || dim > 4096) return set_err(HCR_EINVAL, "dim must be in [1, 4096], got %d", dim);
+  if (dtype != HCR_F16 && dtype != HCR_BF16 && dtype != HCR_F32)
+    return set_err(HCR_EINVAL, "unknown storage dtype %d", dtype);
+  if (capacity_rows < 0) return set_err(HCR_EINVAL, "negative capacity");
+  int ndev = hcr_device_count();
+  if (device < 0 || device >= ndev)
+    return set_err(HCR_EINVAL, "device %d not available (%d HIP devices)", device, ndev);
+  HIPC(hipSetDevice(device));
+  hcr_index* ix = new hcr_index();
+  ix->device = device;
+  ix->dim = dim;
+  ix->ld = (int)round_up(dim, BK);
+  ix->dtype = dtype;
+  hipError_t e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ix;
+    return set_err(HCR_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  int rc = ix->rho.ensure(16);
+  if (rc == HCR_OK) {
+    hipError_t e2 = hipMemset(ix->rho.p, 0, 16);
+    if (e2 != hipSuccess) rc = set_err(HCR_EHIP, "hipMemset: %s", hipGetErrorString(e2));
+  }
+  if (rc != HCR_OK) {
+    hcr_index_destroy(ix);
+    return rc;
+  }
+  *out = ix;
+  if (capacity_rows > 0) {
+    // reserve by growing to the capacity (rows stay empty)
+    rc = hcr_reserve_internal(ix, capacity_rows);
+    if (rc != HCR_OK) {
+      hcr_index_destroy(ix);
+      *out = nullptr;
+      return rc;
+    }
+  }
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_destroy(hcr_index* ix) {
+  if (!ix) return HCR_OK;
+  (void)hipSetDevice(ix->device);
+  if (ix->stream) (void)hipStreamSynchronize(ix->stream);
+  DevBuf* all[] = {&ix->rows, &ix->norm64, &ix->inv32, &ix->maskbits, &ix->rho,
+                   &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
+                   &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
+                   &ix->w_unc, &ix->w_cnt};
+  for (DevBuf* b : all) b->release();
+  if (ix->ev0) (void)hipEventDestroy(ix->ev0);
+  if (ix->ev1) (void)hipEventDestroy(ix->ev1);
+  if (ix->stream) (void)hipStreamDestroy(ix->stream);
+  delete ix;
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_reset(hcr_index* ix) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  HIPC(hipSetDevice(ix->device));
+  HIPC(hipStreamSynchronize(ix->stream));
+  ix->n = 0;
+  ix->has_mask = false;
+  ix->rho_dirty = true;
+  HIPC(hipMemset(ix->rho.p, 0, 16));
+  if (ix->cap > 0) HIPC(hipMemset(ix->maskbits.p, 0xFF, (size_t)(ix->cap / 32) * 4));
+  return HCR_OK;
+}
+
+static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows) {
+  if (want_rows <= ix->cap) return HCR_OK;
+  int64_t ncap = std::max<int64_t>(want_rows, ix->cap + ix->cap / 2);
+  ncap = round_up(std::max<int64_t>(ncap, 128), 128);
+  const size_t es = dtype_size(ix->dtype);
+  DevBuf nrows, nn64, ninv, nmask;
+  CHECK(nrows.ensure((size_t)ncap * ix->ld * es));
+  CHECK(nn64.ensure((size_t)ncap * 8));
+  CHECK(ninv.ensure((size_t)ncap * 4));
+  CHECK(nmask.ensure((size_t)(ncap / 32) * 4));
+  HIPC(hipMemsetAsync(ninv.p, 0, (size_t)ncap * 4, ix->stream));
+  HIPC(hipMemsetAsync(nmask.p, 0xFF, (size_t)(ncap / 32) * 4, ix->stream));
+  if (ix->n > 0) {
+    HIPC(hipMemcpyAsync(nrows.p, ix->rows.p, (size_t)ix->n * ix->ld * es, hipMemcpyDeviceToDevice, ix->stream));
+    HIPC(hipMemcpyAsync(nn64.p, ix->norm64.p, (size_t)ix->n * 8, hipMemcpyDeviceToDevice, ix->stream));
+    HIPC(hipMemcpyAsync(ninv.p, ix->inv32.p, (size_t)ix->n * 4, hipMemcpyDeviceToDevice, ix->stream));
+    if (ix->has_mask)
+      HIPC(hipMemcpyAsync(nmask.p, ix->maskbits.p, (size_t)(ix->cap / 32) * 4, hipMemcpyDeviceToDevice, ix->stream));
+  }
+  HIPC(hipStreamSynchronize(ix->stream));
+  ix->rows.release(); ix->norm64.release(); ix->inv32.release(); ix->maskbits.release();
+  ix->rows = nrows; ix->norm64 = nn64; ix->inv32 = ninv; ix->maskbits = nmask;
+  nrows.p = nn64.p = ninv.p = nmask.p = nullptr;   // ownership moved
+  ix->cap = ncap;
+  return HCR_OK;
+}
+
+template <typename TIN, typename TS>
+static void launch_ingest(hcr_index* ix, const void* d_in, int64_t n, int normalize,
+                          hipStream_t st) {
+  TS* dst = ix->rows.as<TS>() + ix->n * ix->ld;
+  const unsigned grid = (unsigned)((n + 3) / 4);
+  hipLaunchKernelGGL((ingest_kernel<TIN, TS>), dim3(grid), dim3(256), 0, st,
+                     reinterpret_cast<const TIN*>(d_in), n, ix->dim, ix->ld, normalize, dst,
+                     ix->norm64.as<double>() + ix->n, ix->inv32.as<float>() + ix->n,
+                     ix->rho.as<unsigned int>());
+}
+
+static int ingest_device(hcr_index* ix, const void* d_rows, int64_t n, int in_dt, int normalize,
+                         hipStream_t st) {
+  if (in_dt != HCR_F16 && in_dt != HCR_BF16 && in_dt != HCR_F32)
+    return set_err(HCR_EINVAL, "unknown rows dtype %d", in_dt);
+#define ING(TIN, TS) launch_ingest<TIN, TS>(ix, d_rows, n, normalize, st)
+  const int sd = ix->dtype;
+  if (in_dt == HCR_F32) {
+    if (sd == HCR_F16) ING(float, _Float16); else if (sd == HCR_BF16) ING(float, __bf16); else ING(float, float);
+  } else if (in_dt == HCR_F16) {
+    if (sd == HCR_F16) ING(_Float16, _Float16); else if (sd == HCR_BF16) ING(_Float16, __bf16); else ING(_Float16, float);
+  } else {
+    if (sd == HCR_F16) ING(__bf16, _Float16); else if (sd == HCR_BF16) ING(__bf16, __bf16); else ING(__bf16, float);
+  }
+#undef ING
+  HIPC(hipGetLastError());
+  ix->n += n;
+  ix->rho_dirty = true;
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_add_device(hcr_index* ix, const void* d_rows, int64_t n, int rows_dtype,
+                                    int normalize, void* stream) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (n < 0) return set_err(HCR_EINVAL, "negative row count");
+  if (n == 0) return HCR_OK;
+  if (!d_rows) return set_err(HCR_EINVAL, "rows is NULL");
+  if (ix->n + n > (int64_t)0xFFFFFFFEll) return set_err(HCR_EINVAL, "index limited to 2^32-2 rows per shard");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(hcr_reserve_internal(ix, ix->n + n));
+  hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+  if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
+  return ingest_device(ix, d_rows, n, rows_dtype, normalize, st);
+}
+
+extern "C" int hcr_index_add(hcr_index* ix, const void* rows, int64_t n, int rows_dtype,
+                             int normalize) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (n < 0) return set_err(HCR_EINVAL, "negative row count");
+  if (n == 0) return HCR_OK;
+  if (!rows) return set_err(HCR_EINVAL, "rows is NULL");
+  if (rows_dtype != HCR_F16 && rows_dtype != HCR_BF16 && rows_dtype != HCR_F32)
+    return set_err(HCR_EINVAL, "unknown rows dtype %d", rows_dtype);
+  if (ix->n + n > (int64_t)0xFFFFFFFEll) return set_err(HCR_EINVAL, "index limited to 2^32-2 rows per shard");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(hcr_reserve_internal(ix, ix->n + n));
+  const size_t rb = (size_t)ix->dim * dtype_size(rows_dtype);
+  const int64_t chunk = std::max<int64_t>(1, (int64_t)((256u << 20) / rb));
+  for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+    const int64_t m = std::min(chunk, n - r0);
+    CHECK(ix->w_qin.ensure((size_t)m * rb));
+    HIPC(hipMemcpyAsync(ix->w_qin.p, (const char*)rows + (size_t)r0 * rb, (size_t)m * rb,
+                        hipMemcpyHostToDevice, ix->stream));
+    CHECK(ingest_device(ix, ix->w_qin.p, m, rows_dtype, normalize, ix->stream));
+  }
+  HIPC(hipStreamSynchronize(ix->stream));
+  return HCR_OK;
+}
+
+extern "C" int64_t hcr_index_size(const hcr_index* ix) { return ix ? ix->n : -1; }
+extern "C" int hcr_index_dim(const hcr_index* ix) { return ix ? ix->dim : -1; }
+extern "C" int hcr_index_dtype(const hcr_index* ix) { return ix ? ix->dtype : -1; }
+
+extern "C" int hcr_index_set_id_offset(hcr_index* ix, int64_t off) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (off < 0) return set_err(HCR_EINVAL, "negative id offset");
+  ix->id_offset = off;
+  return HCR_OK;
+}
+
+static float half_to_float(uint16_t h) {
+  const uint32_t s = (uint32_t)(h & 0x8000) << 16;
+  uint32_t e = (h >> 10) & 0x1F, m = h & 0x3FF;
+  uint32_t bits;
+  if (e == 0) {
+    if (m == 0) bits = s;
+    else {
+      int sh = 0;
+      while (!(m & 0x400)) { m <<= 1; ++sh; }
+      m &= 0x3FF;
+      bits = s | ((uint32_t)(127 - 15 - sh + 1) << 23) | (m << 13);
+    }
+  } else if (e == 31) {
+    bits = s | 0x7F800000u | (m << 13);
+  } else {
+    bits = s | ((e - 15 + 127) << 23) | (m << 13);
+  }
+  float f;
+  memcpy(&f, &bits, 4);
+  return f;
+}
+
+extern "C" int hcr_index_get_rows(const hcr_index* ix, int64_t row0, int64_t n, float* out) {
+  if (!ix || !out) return set_err(HCR_EINVAL, "NULL argument");
+  if (row0 < 0 || n < 0 || row0 + n > ix->n) return set_err(HCR_EINVAL, "row range out of bounds");
+  if (n == 0) return HCR_OK;
+  HIPC(hipSetDevice(ix->device));
+  const size_t es = dtype_size(ix->dtype);
+  std::vector<char> tmp((size_t)n * ix->ld * es);
+  HIPC(hipStreamSynchronize(ix->stream));
+  HIPC(hipMemcpy(tmp.data(), (const char*)ix->rows.p + (size_t)row0 * ix->ld * es, tmp.size(),
+                 hipMemcpyDeviceToHost));
+  for (int64_t r = 0; r < n; ++r) {
+    for (int d = 0; d < ix->dim; ++d) {
+      const size_t i = (size_t)r * ix->ld + d;
+      float v;
+      if (ix->dtype == HCR_F32) memcpy(&v, tmp.data() + i * 4, 4);
+      else {
+        uint16_t h;
+        memcpy(&h, tmp.data() + i * 2, 2);
+        if (ix->dtype == HCR_F16) v = half_to_float(h);
+        else { uint32_t b = (uint32_t)h << 16; memcpy(&v, &b, 4); }
+      }
+      out[(size_t)r * ix->dim + d] = v;
+    }
+  }
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_set_rowmask(hcr_index* ix, const uint8_t* mask, int64_t n) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  HIPC(hipSetDevice(ix->device));
+  if (!mask) { ix->has_mask = false; return HCR_OK; }
+  if (n != ix->n) return set_err(HCR_EINVAL, "mask length %lld != index size %lld", (long long)n, (long long)ix->n);
+  if (ix->cap == 0) { ix->has_mask = false; return HCR_OK; }
+  std::vector<uint32_t> bits((size_t)(ix->cap / 32), 0u);
+  for (int64_t i = 0; i < n; ++i)
+    if (mask[i]) bits[(size_t)(i >> 5)] |= 1u << (i & 31);
+  HIPC(hipMemcpyAsync(ix->maskbits.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ix->stream));
+  HIPC(hipStreamSynchronize(ix->stream));
+  ix->has_mask = true;
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_set_timing(hcr_index* ix, int enable) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  HIPC(hipSetDevice(ix->device));
+  if (enable && !ix->ev0) {
+    HIPC(hipEventCreate(&ix->ev0));
+    HIPC(hipEventCreate(&ix->ev1));
+  }
+  ix->timing = enable != 0;
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_last_stats(const hcr_index* ix, hcr_search_stats* out) {
+  if (!ix || !out) return set_err(HCR_EINVAL, "NULL argument");
+  *out = ix->stats;
+  return HCR_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// search pipeline
+// ---------------------------------------------------------------------------------------
+static int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
+static constexpr int kMaxKprime = 512;
+static constexpr int kMergeMaxKeys = 8192;      // 64 KiB of LDS in merge_partials_kernel
+static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
+
+static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
+static int cap_for(int kp) { return next_pow2(kp + BR); }
+
+template <typename TS, typename TM, int CAP>
+static void launch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
+  const int nwg = nqb * P;
+  hipLaunchKernelGGL((score_topk_kernel<TS, TM, CAP>), dim3(nwg), dim3(NT), 0, st,
+                     ix->rows.as<const TS>(), ix->ld, ix->n, ix->ld / BK, ix->inv32.as<const float>(),
+                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                     ix->w_qhat.as<const TM>(), nqb, P, ntiles, ix->w_buf.as<uint64_t>(),
+                     ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), kp);
+}
+
+template <typename TS, typename TM>
+static int dispatch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, int cap, hipStream_t st) {
+  switch (cap) {
+    case 256: launch_score<TS, TM, 256>(ix, nqb, P, ntiles, kp, st); break;
+    case 512: launch_score<TS, TM, 512>(ix, nqb, P, ntiles, kp, st); break;
+    case 1024: launch_score<TS, TM, 1024>(ix, nqb, P, ntiles, kp, st); break;
+    default: return set_err(HCR_EINVAL, "internal: unsupported candidate capacity %d", cap);
+  }
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+template <typename TS>
+static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d_q, int nq, int kp, int k, int mode,
+                           double thr, double* out_s, int64_t* out_i, hipStream_t st) {
+  const size_t lds = (size_t)ix->dim * 8 + (size_t)kp * 24 + 16;
+  hipLaunchKernelGGL((rescore_kernel<TS>), dim3(nq), dim3(256), lds, st, merged,
+                     kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
+                     ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
+                     ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>());
+}
+
+// One pipeline pass over nq (<= kQueryChunk) device queries at candidate depth kp.
+// Returns the number of uncertified queries in *n_unc (stream is synchronised).
+static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode, double thr,
+                       double* d_out_s, int64_t* d_out_i, int kp, hipStream_t st, int* n_unc,
+                       std::vector<int>* unc_list) {
+  const uint64_t* merged_ptr = nullptr;
+  const int nqpad = (int)round_up(nq, BQ);
+  const int nqb = nqpad / BQ;
+  const int ntiles = (int)((ix->n + BR - 1) / BR);
+  const int cap = cap_for(kp);
+  int P = std::max(1, (512 + nqb - 1) / nqb);
+  P = std::min(P, ntiles);
+  const int nwg = nqb * P;
+  const bool tm_f16 = ix->dtype == HCR_F16;
+  const size_t tms = 2;
+
+  CHECK(ix->w_qhat.ensure((size_t)nqpad * ix->ld * tms));
+  CHECK(ix->w_qnorm.ensure((size_t)nqpad * 8));
+  CHECK(ix->w_eps.ensure((size_t)nqpad * 8));
+  CHECK(ix->w_taug.ensure((size_t)nqpad * 4));
+  CHECK(ix->w_buf.ensure((size_t)nwg * BQ * cap * 8));
+  CHECK(ix->w_part.ensure((size_t)nqpad * P * kp * 8));
+  const int G = std::max(2, kMergeMaxKeys / kp);            // partitions merged per block
+  const int P2 = (P + G - 1) / G;
+  CHECK(ix->w_merged.ensure((size_t)nqpad * std::max(P2, 1) * kp * 8 * 2));
+  CHECK(ix->w_unc.ensure((size_t)nqpad * 4));
+  CHECK(ix->w_cnt.ensure(16));
+
+  HIPC(hipMemsetAsync(ix->w_qhat.p, 0, (size_t)nqpad * ix->ld * tms, st));
+  HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
+  HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
+
+  // rigorous accumulation bound: gamma_{ld+1} + 4u (u = 2^-24)
+  const double u = std::ldexp(1.0, -24);
+  const double nu = (ix->ld + 1) * u;
+  const double gamma_u = nu / (1.0 - nu) + 4.0 * u;
+  if (ix->rho_dirty) {
+    unsigned int rho_bits = 0;
+    HIPC(hipStreamSynchronize(ix->stream));
+    HIPC(hipMemcpy(&rho_bits, ix->rho.p, 4, hipMemcpyDeviceToHost));
+    float rho_f;
+    memcpy(&rho_f, &rho_bits, 4);
+    ix->rho_host = (double)rho_f;
+    ix->rho_dirty = false;
+  }
+  const double rho = ix->rho_host;
+
+  const unsigned gq = (unsigned)((nq + 3) / 4);
+  if (tm_f16)
+    hipLaunchKernelGGL((prep_queries_kernel<_Float16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
+                       ix->ld, ix->w_qhat.as<_Float16>(), ix->w_qnorm.as<double>(),
+                       ix->w_eps.as<double>(), rho, gamma_u);
+  else
+    hipLaunchKernelGGL((prep_queries_kernel<__bf16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
+                       ix->ld, ix->w_qhat.as<__bf16>(), ix->w_qnorm.as<double>(),
+                       ix->w_eps.as<double>(), rho, gamma_u);
+  HIPC(hipGetLastError());
+
+  if (ix->timing) HIPC(hipEventRecord(ix->ev0, st));
+  if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
+  else if (ix->dtype == HCR_BF16) CHECK((dispatch_score<__bf16, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
+  else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
+  if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
+
+  // tree merge: groups of G partition lists -> one list, until one list per query remains
+  {
+    const uint64_t* src = ix->w_part.as<const uint64_t>();
+    uint64_t* bufs[2] = {ix->w_merged.as<uint64_t>(),
+                         ix->w_merged.as<uint64_t>() + (size_t)nqpad * std::max(P2, 1) * kp};
+    int which = 0, pin = P;
+    while (true) {
+      const int pout = (pin + G - 1) / G;
+      const int M = next_pow2(std::min(G, pin) * kp);
+      uint64_t* dst = bufs[which];
+      hipLaunchKernelGGL(merge_partials_kernel, dim3(nq, pout), dim3(256), (size_t)M * 8, st,
+                         src, pin, G, kp, M, dst);
+      HIPC(hipGetLastError());
+      src = dst;
+      which ^= 1;
+      if (pout == 1) break;
+      pin = pout;
+    }
+    merged_ptr = src;
+  }
+
+  if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+  else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+  else launch_rescore<float>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+  HIPC(hipGetLastError());
+
+  int cnt = 0;
+  HIPC(hipMemcpyAsync(&cnt, ix->w_cnt.p, 4, hipMemcpyDeviceToHost, st));
+  HIPC(hipStreamSynchronize(st));
+  *n_unc = cnt;
+  if (ix->stats.partitions == 0) {
+    ix->stats.partitions = P;
+    ix->stats.workgroups = nwg;
+  }
+  if (ix->timing) {
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+    ix->stats.score_kernel_ms += ms;
+    ix->stats.score_launches += 1;
+  }
+  if (cnt > 0 && unc_list) {
+    std::vector<int> flags(nq);
+    HIPC(hipMemcpy(flags.data(), ix->w_unc.p, (size_t)nq * 4, hipMemcpyDeviceToHost));
+    unc_list->clear();
+    for (int i = 0; i < nq; ++i)
+      if (flags[i]) unc_list->push_back(i);
+  }
+  return HCR_OK;
+}
+
+// Full search of nq device queries with certificate widening.
+static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k, int mode,
+                              double thr, double* d_out_s, int64_t* d_out_i, hipStream_t st) {
+  ix->stats = hcr_search_stats{};
+  if (nq == 0) return HCR_OK;
+  if (ix->n == 0) {
+    const int64_t tot = nq * (int64_t)k;
+    hipLaunchKernelGGL(fill_empty, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, d_out_s,
+                       d_out_i, tot);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+    return HCR_OK;
+  }
+  const int kp0 = choose_kprime(k);
+  ix->stats.kprime = kp0;
+  for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
+    const int m = (int)std::min<int64_t>(kQueryChunk, nq - q0);
+    const float* qc = d_q + q0 * ix->dim;
+    double* os = d_out_s + q0 * k;
+    int64_t* oi = d_out_i + q0 * k;
+    int n_unc = 0;
+    std::vector<int> unc;
+    CHECK(search_pass(ix, qc, m, k, mode, thr, os, oi, kp0, st, &n_unc, &unc));
+    int kp = kp0;
+    while (n_unc > 0 && kp < kMaxKprime) {
+      kp = std::min(kMaxKprime, kp * 4);
+      ix->stats.widened_queries += n_unc;
+      const int nu = (int)unc.size();
+      DevBuf idx, qsub, ssub, isub;
+      CHECK(idx.ensure((size_t)nu * 4));
+      CHECK(qsub.ensure((size_t)nu * ix->dim * 4));
+      CHECK(ssub.ensure((size_t)nu * k * 8));
+      CHECK(isub.ensure((size_t)nu * k * 8));
+      HIPC(hipMemcpyAsync(idx.p, unc.data(), (size_t)nu * 4, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(gather_rows_f32, dim3(nu), dim3(256), 0, st, qc, idx.as<const int>(), nu,
+                         ix->dim, qsub.as<float>());
+      HIPC(hipGetLastError());
+      std::vector<int> unc2;
+      int n2 = 0;
+      int rc = search_pass(ix, qsub.as<const float>(), nu, k, mode, thr, ssub.as<double>(),
+                           isub.as<int64_t>(), kp, st, &n2, &unc2);
+      if (rc == HCR_OK) {
+        hipLaunchKernelGGL(scatter_topk, dim3(nu), dim3(64), 0, st, ssub.as<const double>(),
+                           isub.as<const int64_t>(), idx.as<const int>(), nu, k, os, oi);
+        hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = set_err(HCR_EHIP, "scatter: %s", hipGetErrorString(e));
+      }
+      // map the still-uncertified subset back to chunk-local query indices
+      std::vector<int> mapped;
+      for (int j : unc2) mapped.push_back(unc[j]);
+      idx.release(); qsub.release(); ssub.release(); isub.release();
+      if (rc != HCR_OK) return rc;
+      unc.swap(mapped);
+      n_unc = n2;
+    }
+    ix->stats.uncertified_queries += n_unc;
+  }
+  return HCR_OK;
+}
+
+extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t nq, int k,
+                                 int score_mode, double threshold, double* d_out_scores,
+                                 int64_t* d_out_ids, void* stream) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
+  if (k <= 0 || k > 256) return set_err(HCR_EINVAL, "k must be in [1, 256], got %d", k);
+  if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
+    return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
+  if (nq > 0 && (!d_queries || !d_out_scores || !d_out_ids)) return set_err(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(ix->device));
+  hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+  if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
+  return search_device_impl(ix, d_queries, nq, k, score_mode, threshold, d_out_scores, d_out_ids, st);
+}
+
+extern "C" int hcr_search(hcr_index* ix, const float* queries, int64_t nq, int k, int score_mode,
+                          float threshold, float* out_scores, int64_t* out_ids) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
+  if (k <= 0 || k > 256) return set_err(HCR_EINVAL, "k must be in [1, 256], got %d", k);
+  if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
+    return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
+  if (nq == 0) return HCR_OK;
+  if (!queries || !out_scores || !out_ids) return set_err(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(ix->device));
+  for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
+    const int64_t m = std::min<int64_t>(kQueryChunk, nq - q0);
+    CHECK(ix->w_qin.ensure((size_t)m * ix->dim * 4));
+    CHECK(ix->w_outs.ensure((size_t)m * k * 8));
+    CHECK(ix->w_outi.ensure((size_t)m * k * 8));
+    HIPC(hipMemcpyAsync(ix->w_qin.p, queries + q0 * ix->dim, (size_t)m * ix->dim * 4,
+                        hipMemcpyHostToDevice, ix->stream));
+    CHECK(search_device_impl(ix, ix->w_qin.as<const float>(), m, k, score_mode, (double)threshold,
+                             ix->w_outs.as<double>(), ix->w_outi.as<int64_t>(), ix->stream));
+    std::vector<double> s((size_t)m * k);
+    HIPC(hipMemcpy(s.data(), ix->w_outs.p, s.size() * 8, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(out_ids + q0 * k, ix->w_outi.p, s.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < s.size(); ++i) out_scores[q0 * k + i] = (float)s[i];
+  }
+  return HCR_OK;
+}
+
+extern "C" int hcr_score_all(hcr_index* ix, const float* queries, int64_t nq, int score_mode,
+                             double* out_scores) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
+  if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
+    return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
+  if (nq == 0 || ix->n == 0) return HCR_OK;
+  if (!queries || !out_scores) return set_err(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(ix->device));
+  const int64_t qc = 1024;
+  for (int64_t q0 = 0; q0 < nq; q0 += qc) {
+    const int m = (int)std::min<int64_t>(qc, nq - q0);
+    CHECK(ix->w_qin.ensure((size_t)m * ix->dim * 4));
+    CHECK(ix->w_qnorm.ensure((size_t)m * 8));
+    CHECK(ix->w_outs.ensure((size_t)m * ix->n * 8));
+    HIPC(hipMemcpyAsync(ix->w_qin.p, queries + q0 * ix->dim, (size_t)m * ix->dim * 4,
+                        hipMemcpyHostToDevice, ix->stream));
+    hipLaunchKernelGGL(query_norms_kernel, dim3((m + 3) / 4), dim3(256), 0, ix->stream,
+                       ix->w_qin.as<const float>(), m, ix->dim, ix->w_qnorm.as<double>());
+    dim3 grid((unsigned)((ix->n + 3) / 4), (unsigned)m);
+#define EXA(TS)                                                                              \
+  hipLaunchKernelGGL((exact_all_kernel<TS>), grid, dim3(256), 0, ix->stream,                 \
+                     ix->w_qin.as<const float>(), ix->dim, ix->w_qnorm.as<const double>(),   \
+                     ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), \
+                     score_mode, ix->w_outs.as<double>())
+    if (ix->dtype == HCR_F16) EXA(_Float16); else if (ix->dtype == HCR_BF16) EXA(__bf16); else EXA(float);
+#undef EXA
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(out_scores + q0 * ix->n, ix->w_outs.p, (size_t)m * ix->n * 8,
+                        hipMemcpyDeviceToHost, ix->stream));
+    HIPC(hipStreamSynchronize(ix->stream));
+  }
+  return HCR_OK;
+}
+
+extern "C" int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g,
+                                     int64_t nq, int k, double* d_out_scores, int64_t* d_out_ids,
+                                     void* stream) {
+  if (g <= 0 || k <= 0 || nq < 0) return set_err(HCR_EINVAL, "bad merge shape g=%d k=%d", g, k);
+  if ((int64_t)g * k > 8192) return set_err(HCR_EINVAL, "g*k must be <= 8192");
+  if (nq == 0) return HCR_OK;
+  if (!d_scores || !d_ids || !d_out_scores || !d_out_ids) return set_err(HCR_EINVAL, "NULL buffer");
+  const int M = next_pow2(g * k);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(merge_shards_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 16, st,
+                     d_scores, d_ids, g, nq, k, M, d_out_scores, d_out_ids);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}

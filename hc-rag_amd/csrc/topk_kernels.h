@@ -1,0 +1,633 @@
+// topk_kernels.h — HIP kernels of the brute-force cosine top-k path.
+//
+// Pipeline for one query batch (all kernels on one stream):
+//   K0 ingest_kernel         rows -> storage dtype (+ optional fp64 L2 normalisation),
+//                            per-row fp64 norm, fp32 inverse norm, quantisation bound rho.
+//   K1 prep_queries_kernel   fp32 queries -> fp64 norm, MFMA-dtype unit query q^, and the
+//                            rigorous per-query bound eps_q >= |coarse - exact|.
+//   K2 score_topk_kernel     fused MFMA GEMM (corpus tile x query block) + per-query top-k'
+//                            epilogue: never materialises the B x N score matrix.
+//   K3 merge_partials_kernel per query, P partition lists of k' keys -> global top-k' keys.
+//   K4 rescore_kernel        fp64 exact cosine of the k' candidates, (score desc, id asc)
+//                            sort, certificate  c_k' + eps_q < s_k, top-k + mode + threshold.
+//   K5 merge_shards_kernel   g row-shards' exact top-k lists -> global top-k (multi-GPU).
+#pragma once
+#include "device_common.h"
+
+namespace hcr {
+
+constexpr int BR = 128;       // corpus rows per tile
+constexpr int BQ = 128;       // queries per block
+constexpr int BK = 64;        // K (embedding dim) per stage
+constexpr int NT = 256;       // threads per workgroup (4 waves, 2x2 over rows x queries)
+constexpr int STAGE_BYTES = (BR + BQ) * BK * 2;   // 32 KiB: A (rows) 16 KiB + B (queries) 16 KiB
+constexpr int LDS_STAGES = 2 * STAGE_BYTES;        // double buffered
+
+template <typename T> struct MfmaOp;
+template <> struct MfmaOp<_Float16> {
+  using V = half8;
+  static __device__ __forceinline__ floatx4 run(V a, V b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct MfmaOp<__bf16> {
+  using V = bf16x8;
+  static __device__ __forceinline__ floatx4 run(V a, V b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+
+// -------------------------------------------------------------------------------------
+// K0: ingest. One wave per row.
+// -------------------------------------------------------------------------------------
+template <typename TIN, typename TS>
+__global__ void __launch_bounds__(256)
+ingest_kernel(const TIN* __restrict__ in, int64_t n, int dim, int ld, int normalize,
+              TS* __restrict__ out_rows, double* __restrict__ norm64, float* __restrict__ inv32,
+              unsigned int* __restrict__ rho_bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const TIN* src = in + row * dim;
+  double scale = 1.0;
+  if (normalize) {
+    double ss = 0.0;
+    for (int d = lane; d < dim; d += 64) { const double x = (double)to_f32(src[d]); ss += x * x; }
+    ss = wave_sum_f64(ss);
+    const double nr = sqrt(ss);
+    scale = (nr < 10.0 * 2.220446049250313e-16) ? 1.0 : 1.0 / nr;
+  }
+  double ss2 = 0.0, q2 = 0.0;
+  TS* dst = out_rows + row * (int64_t)ld;
+  for (int d = lane; d < ld; d += 64) {
+    const double x = d < dim ? (double)to_f32(src[d]) * scale : 0.0;
+    const TS v = (TS)(float)x;
+    dst[d] = v;
+    const double xd = (double)(float)v;
+    ss2 += xd * xd;
+    if constexpr (sizeof(TS) == 2 && __is_same(TS, _Float16)) {
+      // f16 subnormals may be flushed by the MFMA: account for them in rho.
+      if (xd != 0.0 && fabs(xd) < 6.103515625e-05) q2 += xd * xd;
+    } else if constexpr (sizeof(TS) == 4) {
+      // f32 rows enter the MFMA as bf16: per-row relative quantisation error.
+      const double bq = (double)(float)(__bf16)(float)v;
+      q2 += (bq - xd) * (bq - xd);
+    }
+  }
+  ss2 = wave_sum_f64(ss2);
+  q2 = wave_sum_f64(q2);
+  if (lane == 0) {
+    double nr = sqrt(ss2);
+    if (nr < 10.0 * 2.220446049250313e-16) nr = 1.0;
+    norm64[row] = nr;
+    inv32[row] = (float)(1.0 / nr);
+    if (q2 > 0.0) {
+      const float rho = (float)(sqrt(q2) / nr) * 1.0001f;
+      atomicMax(rho_bits, __float_as_uint(rho));
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// K1: query preparation. One wave per query.
+//   q_n = q / ||q||_2 (fp64, sklearn zero rule), q^ = TM(q_n) with f16 subnormals -> 0,
+//   eps = ||q^ - q_n|| + rho*||q^|| + gamma_u*||q^||*(1+rho)   
+//   eps < 0 marks a zero query (all scores exactly 0).
+// -------------------------------------------------------------------------------------
+template <typename TM>
+__global__ void __launch_bounds__(256)
+prep_queries_kernel(const float* __restrict__ q32, int nq, int dim, int ld, TM* __restrict__ qhat,
+                    double* __restrict__ qnorm, double* __restrict__ eps, double rho,
+                    double gamma_u) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  const float* src = q32 + (int64_t)q * dim;
+  double ss = 0.0;
+  for (int d = lane; d < dim; d += 64) { const double x = (double)src[d]; ss += x * x; }
+  ss = wave_sum_f64(ss);
+  double nr = sqrt(ss);
+  const bool zero = !(nr > 0.0);
+  if (nr < 10.0 * 2.220446049250313e-16) nr = 1.0;
+  double d2 = 0.0, h2 = 0.0;
+  TM* dst = qhat + (int64_t)q * ld;
+  for (int d = lane; d < ld; d += 64) {
+    const double x = d < dim ? (double)src[d] / nr : 0.0;
+    TM h = (TM)(float)x;
+    if constexpr (__is_same(TM, _Float16)) {
+      if (fabs(x) < 6.103515625e-05) h = (TM)0.0f;
+    }
+    dst[d] = h;
+    const double hd = (double)(float)h;
+    d2 += (hd - x) * (hd - x);
+    h2 += hd * hd;
+  }
+  d2 = wave_sum_f64(d2);
+  h2 = wave_sum_f64(h2);
+  if (lane == 0) {
+    qnorm[q] = nr;
+    const double delta = sqrt(d2), nh = sqrt(h2);
+    eps[q] = zero ? -1.0 : delta * (1.0 + 1e-9) + rho * nh + gamma_u * nh * (1.0 + rho) + 1e-12;
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// K2 helpers: global -> register -> LDS staging of one 128 x 64 tile (16 KiB, MFMA dtype).
+// LDS image: [row][8 chunks of 16 B], chunk slot = chunk ^ (row & 7)  (conflict-free for
+// the 16x16x32 fragment reads).
+// -------------------------------------------------------------------------------------
+template <typename TS> struct TileLoader;   // corpus rows in storage dtype TS
+
+// 16-bit storage: 4 x 16 B per thread.
+template <typename TS> struct TileLoader {
+  uint4 r[4];
+  __device__ __forceinline__ void load(const TS* __restrict__ base, int64_t row0, int64_t nrows,
+                                       int ld, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int row = c >> 3, ch = c & 7;
+      int64_t gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      r[i] = *reinterpret_cast<const uint4*>(base + gr * ld + k0 + ch * 8);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds_tile, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int row = c >> 3, ch = c & 7;
+      *reinterpret_cast<uint4*>(lds_tile + row * 128 + ((ch ^ (row & 7)) << 4)) = r[i];
+    }
+  }
+};
+// f32 storage: 8 x 16 B per thread, converted to bf16 on the way into LDS.
+template <> struct TileLoader<float> {
+  float4 r[8];
+  __device__ __forceinline__ void load(const float* __restrict__ base, int64_t row0,
+                                       int64_t nrows, int ld, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int row = c >> 3, ch = c & 7;
+      int64_t gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      const float4* p = reinterpret_cast<const float4*>(base + gr * ld + k0 + ch * 8);
+      r[2 * i] = p[0];
+      r[2 * i + 1] = p[1];
+    }
+  }
+  __device__ __forceinline__ void store(char* lds_tile, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + NT * i;
+      const int row = c >> 3, ch = c & 7;
+      bf16x8 v;
+      v[0] = (__bf16)r[2 * i].x; v[1] = (__bf16)r[2 * i].y;
+      v[2] = (__bf16)r[2 * i].z; v[3] = (__bf16)r[2 * i].w;
+      v[4] = (__bf16)r[2 * i + 1].x; v[5] = (__bf16)r[2 * i + 1].y;
+      v[6] = (__bf16)r[2 * i + 1].z; v[7] = (__bf16)r[2 * i + 1].w;
+      *reinterpret_cast<bf16x8*>(lds_tile + row * 128 + ((ch ^ (row & 7)) << 4)) = v;
+    }
+  }
+};
+
+// Wave-cooperative compaction of one query's candidate buffer to its best `kp` keys.
+// Writes the sorted survivors back to `qbuf` (or to `out` when non-null, zero padded to kp),
+// updates the LDS count / local threshold and raises the global threshold.
+template <int CAP>
+__device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ qbuf, int* cnt_q,
+                                              uint64_t* tau_key_q, uint32_t* tau_g_q, int kp,
+                                              int lane, uint64_t* __restrict__ out) {
+  constexpr int E = CAP / 64;
+  const int c = *cnt_q;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int idx = lane * E + e;
+    v[e] = idx < c ? qbuf[idx] : 0ull;
+  }
+  wave_sort_desc<E>(v, lane);
+  const int nk = c < kp ? c : kp;
+  if (out) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int idx = lane * E + e;
+      if (idx < kp) out[idx] = v[e];      // zeros beyond nk
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int idx = lane * E + e;
+      if (idx < nk) qbuf[idx] = v[e];
+    }
+  }
+  uint64_t kth = 0;
+  if (nk == kp) {
+    const int want = kp - 1, src_lane = want / E, src_e = want % E;
+    uint64_t sel = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) sel = (e == src_e) ? v[e] : sel;
+    kth = shfl_u64(sel, src_lane);
+  }
+  if (lane == 0) {
+    *cnt_q = nk;
+    *tau_key_q = kth;
+    if (kth) atomicMax(tau_g_q, (uint32_t)(kth >> 32));
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// K2: fused score + top-k' kernel.
+//   grid  = nqb query blocks x P row partitions (XCD-aware: the nqb blocks sharing one
+//           partition's corpus tiles are dispatched consecutively on one XCD so each corpus
+//           tile is fetched from HBM once and re-read from that XCD's L2).
+//   block = 256 threads = 4 waves in 2 (rows) x 2 (queries); wave tile 64 rows x 64 queries
+//           = 4 x 4 MFMA 16x16x32 accumulators.  C = E_tile . Q_block^T, so each lane holds
+//           4 consecutive rows of ONE query per accumulator (query = lane & 15).
+//   Each workgroup walks its partition's row tiles in ascending order, keeps a private
+//   per-query candidate buffer (global, L2/MALL resident, CAP keys per query) and a local
+//   threshold = its k'-th best key; a global per-query threshold (atomicMax of every
+//   workgroup's local k'-th score, a valid lower bound of the global k'-th score) prunes.
+// -------------------------------------------------------------------------------------
+template <typename TS, typename TM, int CAP>
+__global__ void __launch_bounds__(NT, 2)
+score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
+                  const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
+                  const TM* __restrict__ qhat, int nqb, int P, int ntiles,
+                  uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
+                  uint64_t* __restrict__ partials, int kp) {
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_STAGES + BQ * 8 + BQ * 4 + 16];
+  uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + LDS_STAGES);
+  int* cnt = reinterpret_cast<int*>(lds + LDS_STAGES + BQ * 8);
+  int* flag = reinterpret_cast<int*>(lds + LDS_STAGES + BQ * 12);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int qb = g % nqb, p = g / nqb;
+  const int t0 = (int)((int64_t)p * ntiles / P);
+  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
+  const int qbase = qb * BQ;
+  uint64_t* wbuf = buf + (size_t)b * BQ * CAP;
+
+  for (int i = tid; i < BQ; i += NT) { tau_key[i] = 0ull; cnt[i] = 0; }
+  if (tid == 0) *flag = 0;
+
+  if (t0 >= t1) {
+    for (int i = tid; i < BQ * kp; i += NT) {
+      const int ql = i / kp, j = i - ql * kp;
+      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
+    }
+    return;
+  }
+
+  const TM* qblk = qhat + (size_t)qbase * ld;
+  TileLoader<TS> la;
+  TileLoader<TM> lb;
+
+  // fragment read offsets (bytes inside a tile image)
+  const int lr = lane & 15;
+  const int c0 = (lane >> 4) ^ (lane & 7);       // chunk slot for kk = 0
+  const int offA0 = (wr * 64 + lr) * 128 + (c0 << 4);
+  const int offA1 = (wr * 64 + lr) * 128 + ((c0 ^ 4) << 4);
+  const int offB0 = (wc * 64 + lr) * 128 + (c0 << 4);
+  const int offB1 = (wc * 64 + lr) * 128 + ((c0 ^ 4) << 4);
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: stage 0
+  la.load(rows, (int64_t)t0 * BR, n_rows, ld, 0, tid);
+  lb.load(qblk, 0, (int64_t)BQ, ld, 0, tid);
+  la.store(lds, tid);
+  lb.store(lds + BR * 128, tid);
+  __syncthreads();
+
+  const int nsteps = (t1 - t0) * ksteps;
+  int tile = t0, ks = 0;
+  float4 invv[4];
+  uint4 mw = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+  uint32_t tg[4];
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = (s + 1) < nsteps;
+    int ntile = tile, nks = ks + 1;
+    if (nks == ksteps) { nks = 0; ++ntile; }
+    const bool last_k = (ks == ksteps - 1);
+    if (last_k) {
+      const int64_t row0 = (int64_t)tile * BR;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        invv[m] = *reinterpret_cast<const float4*>(inv_norm + row0 + wr * 64 + m * 16 + (lane >> 4) * 4);
+      if (mask) mw = *reinterpret_cast<const uint4*>(mask + (row0 >> 5));
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        tg[n] = __hip_atomic_load(tau_g + qbase + wc * 64 + n * 16 + lr, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (more) {
+      la.load(rows, (int64_t)ntile * BR, n_rows, ld, nks * BK, tid);
+      lb.load(qblk, 0, (int64_t)BQ, ld, nks * BK, tid);
+    }
+    {
+      const char* sa = lds + cur * STAGE_BYTES;
+      const char* sb = sa + BR * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int oa = kk ? offA1 : offA0;
+        const int ob = kk ? offB1 : offB0;
+        V a[4], bq[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const V*>(sa + oa + m * 16 * 128);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(sb + ob + n * 16 * 128);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(a[m], bq[n], acc[m][n]);
+      }
+    }
+    if (more) {
+      char* st = lds + (cur ^ 1) * STAGE_BYTES;
+      la.store(st, tid);
+      lb.store(st + BR * 128, tid);
+    }
+    __syncthreads();
+
+    if (last_k) {
+      // ------------------------------- epilogue --------------------------------------
+      const int64_t row0 = (int64_t)tile * BR;
+      float thr[4];
+      uint64_t tk[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int ql = wc * 64 + n * 16 + lr;
+        tk[n] = tau_key[ql];
+        const float ls = tk[n] ? key_score(tk[n]) : -INFINITY;
+        thr[n] = fmaxf(ls, unord32(tg[n]));
+      }
+      float iv[4][4];
+      const uint32_t mwa[4] = {mw.x, mw.y, mw.z, mw.w};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int rl = wr * 64 + m * 16 + (lane >> 4) * 4;   // row inside tile
+        const float ivm[4] = {invv[m].x, invv[m].y, invv[m].z, invv[m].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = rl + r;
+          const bool ok = (row0 + rr < n_rows) && ((mwa[rr >> 5] >> (rr & 31)) & 1u);
+          iv[m][r] = ok ? ivm[r] : __builtin_nanf("");
+        }
+      }
+      bool hit[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m][n][r] * iv[m][r]);
+        hit[n] = mx >= thr[n];
+      }
+      if (__any(hit[0] | hit[1] | hit[2] | hit[3])) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          if (hit[n]) {
+            const int ql = wc * 64 + n * 16 + lr;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float sc = acc[m][n][r] * iv[m][r];
+                if (sc >= thr[n]) {
+                  const uint32_t lrow = (uint32_t)(row0 + wr * 64 + m * 16 + (lane >> 4) * 4 + r);
+                  const uint64_t key = make_key(sc, lrow);
+                  if (key > tk[n]) {
+                    const int pos = atomicAdd(&cnt[ql], 1);
+                    wbuf[(size_t)ql * CAP + pos] = key;
+                    if (pos + 1 > CAP - BR) *flag = 1;
+                  }
+                }
+              }
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      __syncthreads();
+      if (*flag) {
+        for (int ql = wave; ql < BQ; ql += 4) {
+          if (cnt[ql] > CAP - BR)
+            compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+                               tau_g + qbase + ql, kp, lane, nullptr);
+        }
+        __syncthreads();
+        if (tid == 0) *flag = 0;
+      }
+    }
+    tile = ntile;
+    ks = nks;
+  }
+
+  // final: every query's best kp keys -> partials[q][p][0..kp)
+  for (int ql = wave; ql < BQ; ql += 4) {
+    compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
+                       lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// K3: merge the P partition lists of one query into its global top-k' (sorted desc).
+// -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+merge_partials_kernel(const uint64_t* __restrict__ lists, int P, int G, int kp, int M,
+                      uint64_t* __restrict__ out) {
+  // lists: [q][P][kp] sorted-or-not key lists; block (q, grp) merges lists [grp*G, grp*G+G)
+  // into out[q][grp][0..kp) sorted descending.
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm_keys[];
+  const int q = blockIdx.x, grp = blockIdx.y, pout = gridDim.y;
+  const int p0 = grp * G;
+  const int np = min(G, P - p0);
+  const uint64_t* src = lists + ((size_t)q * P + p0) * kp;
+  const int tot = np * kp;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) sm_keys[i] = i < tot ? src[i] : 0ull;
+  __syncthreads();
+  block_sort_desc_u64(sm_keys, M);
+  uint64_t* dst = out + ((size_t)q * pout + grp) * kp;
+  for (int i = threadIdx.x; i < kp; i += blockDim.x) dst[i] = sm_keys[i];
+}
+
+// -------------------------------------------------------------------------------------
+// K4: exact fp64 rescoring + certificate + final top-k.
+// -------------------------------------------------------------------------------------
+template <typename TS>
+__global__ void __launch_bounds__(256)
+rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restrict__ q32,
+               int dim, const double* __restrict__ qnorm, const double* __restrict__ eps,
+               const TS* __restrict__ rows, int ld, const double* __restrict__ norm64, int k,
+               int mode, double thr, int64_t id_offset, double* __restrict__ out_s,
+               int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
+               int* __restrict__ unc_count) {
+  extern __shared__ __attribute__((aligned(16))) char sm_raw[];
+  double* qd = reinterpret_cast<double*>(sm_raw);
+  uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
+  uint64_t* lo = hi + kp;
+  uint64_t* keys = lo + kp;
+  int& s_nvalid = *reinterpret_cast<int*>(keys + kp);   // all LDS in the dynamic region
+  const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* src = q32 + (int64_t)q * dim;
+  for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];
+  for (int c = threadIdx.x; c < kp; c += blockDim.x) keys[c] = merged[(size_t)q * kp + c];
+  if (threadIdx.x == 0) s_nvalid = 0;
+  __syncthreads();
+  const double qn = qnorm[q];
+  for (int c = wave; c < kp; c += 4) {
+    const uint64_t key = keys[c];
+    if (key == 0ull) {
+      if (lane == 0) { hi[c] = 0ull; lo[c] = 0ull; }
+      continue;
+    }
+    const uint32_t row = key_row(key);
+    const TS* e = rows + (int64_t)row * ld;
+    double acc = 0.0;
+    for (int d = lane; d < dim; d += 64) acc += qd[d] * (double)(float)e[d];
+    acc = wave_sum_f64(acc);
+    if (lane == 0) {
+      const double s = acc / (qn * norm64[row]);
+      hi[c] = ord64(s);
+      lo[c] = (uint64_t)(0xFFFFFFFFu - row);
+      atomicAdd(&s_nvalid, 1);
+    }
+  }
+  __syncthreads();
+  block_sort_desc_pair(hi, lo, kp);
+  const int nvalid = s_nvalid;
+  if (threadIdx.x == 0) {
+    bool cert = true;
+    const double e = eps[q];
+    if (nvalid >= kp && e >= 0.0) {   // e < 0: zero query, exact scores are all 0
+      const double ckp = (double)key_score(keys[kp - 1]);
+      const double sk = unord64(hi[k - 1]);
+      cert = ckp + e < sk;
+    }
+    unc_flags[q] = cert ? 0 : 1;
+    if (!cert) atomicAdd(unc_count, 1);
+  }
+  for (int t = threadIdx.x; t < k; t += blockDim.x) {
+    double s = -INFINITY;
+    int64_t id = -1;
+    if (t < nvalid) {
+      double v = unord64(hi[t]);
+      if (mode == 1) v = (v + 1.0) / 2.0;
+      if (v >= thr) { s = v; id = id_offset + (int64_t)(0xFFFFFFFFu - (uint32_t)lo[t]); }
+    }
+    out_s[(size_t)q * k + t] = s;
+    out_i[(size_t)q * k + t] = id;
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// exact fp64 scores of every (query, row) pair (small indexes; isRelevant a1 semantics)
+// -------------------------------------------------------------------------------------
+template <typename TS>
+__global__ void __launch_bounds__(256)
+exact_all_kernel(const float* __restrict__ q32, int dim, const double* __restrict__ qnorm,
+                 const TS* __restrict__ rows, int ld, int64_t n,
+                 const double* __restrict__ norm64, int mode, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = blockIdx.y;
+  if (row >= n) return;
+  const float* qs = q32 + (int64_t)q * dim;
+  const TS* e = rows + row * ld;
+  double acc = 0.0;
+  for (int d = lane; d < dim; d += 64) acc += (double)qs[d] * (double)(float)e[d];
+  acc = wave_sum_f64(acc);
+  if (lane == 0) {
+    double s = acc / (qnorm[q] * norm64[row]);
+    if (mode == 1) s = (s + 1.0) / 2.0;
+    out[(int64_t)q * n + row] = s;
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// K5: merge g shards' top-k lists ([g][nq][k], exact fp64 scores, -1 = empty).
+// -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+merge_shards_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g,
+                    int64_t nq, int k, int M, double* __restrict__ out_s,
+                    int64_t* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm_pair[];
+  uint64_t* hi = sm_pair;
+  uint64_t* lo = sm_pair + M;
+  const int64_t q = blockIdx.x;
+  const int tot = g * k;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    uint64_t h = 0ull, l = 0ull;
+    if (i < tot) {
+      const int j = i / k, c = i - j * k;
+      const size_t off = ((size_t)j * nq + q) * k + c;
+      const int64_t id = ids[off];
+      if (id >= 0) { h = ord64(s[off]); l = ~(uint64_t)id; }
+    }
+    hi[i] = h;
+    lo[i] = l;
+  }
+  __syncthreads();
+  block_sort_desc_pair(hi, lo, M);
+  for (int t = threadIdx.x; t < k; t += blockDim.x) {
+    const bool ok = hi[t] != 0ull;
+    out_s[q * k + t] = ok ? unord64(hi[t]) : -INFINITY;
+    out_i[q * k + t] = ok ? (int64_t)(~lo[t]) : -1;
+  }
+}
+
+// gather / scatter helpers for certificate widening
+__global__ void gather_rows_f32(const float* __restrict__ src, const int* __restrict__ idx, int n,
+                                int dim, float* __restrict__ dst) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const float* s = src + (int64_t)idx[i] * dim;
+  float* d = dst + (int64_t)i * dim;
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) d[j] = s[j];
+}
+__global__ void scatter_topk(const double* __restrict__ s, const int64_t* __restrict__ ids,
+                             const int* __restrict__ idx, int n, int k, double* __restrict__ out_s,
+                             int64_t* __restrict__ out_i) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  for (int j = threadIdx.x; j < k; j += blockDim.x) {
+    out_s[(int64_t)idx[i] * k + j] = s[(int64_t)i * k + j];
+    out_i[(int64_t)idx[i] * k + j] = ids[(int64_t)i * k + j];
+  }
+}
+__global__ void fill_empty(double* __restrict__ s, int64_t* __restrict__ ids, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { s[i] = -INFINITY; ids[i] = -1; }
+}
+__global__ void query_norms_kernel(const float* __restrict__ q32, int nq, int dim,
+                                   double* __restrict__ qnorm) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  double ss = 0.0;
+  for (int d = lane; d < dim; d += 64) { const double x = (double)q32[(int64_t)q * dim + d]; ss += x * x; }
+  ss = wave_sum_f64(ss);
+  if (lane == 0) { double nr = sqrt(ss); qnorm[q] = nr < 10.0 * 2.220446049250313e-16 ? 1.0 : nr; }
+}
+
+}  // namespace hcr

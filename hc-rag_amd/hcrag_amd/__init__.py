@@ -1,0 +1,17 @@
+"""hcrag_amd — MI355X-native embedding + vector-retrieval core for HC-RAG's hot path.
+
+Host package over libhcrag_hip.so (HIP, gfx950).  See DESIGN.md for the architecture and
+INTEGRATION.md for the drop-in points in the reference (graph_builder.py:146-161,
+query_interface.py:136-139,172-204, experiments/main.py:831-905,
+experiments/isRelevant.py:197-210).
+"""
+from ._lib import (HCR_BF16, HCR_F16, HCR_F32, HCR_SCORE_COSINE, HCR_SCORE_UNIT, HcrError,
+                   device_count, lib)
+from .index import VectorIndex, merge_topk_device
+from .retrieval import EmbeddingSearch, batch_semantic_similarity
+
+__version__ = "0.1.0"
+
+__all__ = ["VectorIndex", "merge_topk_device", "EmbeddingSearch", "batch_semantic_similarity",
+           "device_count", "lib", "HcrError", "HCR_F16", "HCR_BF16", "HCR_F32",
+           "HCR_SCORE_COSINE", "HCR_SCORE_UNIT"]

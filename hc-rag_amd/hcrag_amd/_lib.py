@@ -1,0 +1,104 @@
+"""ctypes binding of libhcrag_hip.so (C ABI declared in include/hcrag.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be loaded,
+``lib()`` raises.  (The CPU restatement under ``oracle/`` is test infrastructure only.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_uint8, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "HCRAG_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libhcrag_hip.so"))
+
+HCR_OK, HCR_EINVAL, HCR_EHIP, HCR_ERCCL, HCR_ENOMEM, HCR_EIO = 0, -1, -2, -3, -4, -5
+HCR_F16, HCR_BF16, HCR_F32 = 0, 1, 2
+HCR_SCORE_COSINE, HCR_SCORE_UNIT = 0, 1
+
+
+class HcrError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"hcrag error {code}: {msg}")
+        self.code = code
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("kprime", c_int32), ("widened_queries", c_int32),
+                ("uncertified_queries", c_int32), ("partitions", c_int32),
+                ("score_launches", c_int32), ("workgroups", c_int32),
+                ("score_kernel_ms", c_double)]
+
+
+class BertConfig(ctypes.Structure):
+    """Mirror of ``hcr_bert_config`` (include/hcrag.h)."""
+    _fields_ = [("vocab_size", c_int32), ("hidden", c_int32), ("layers", c_int32),
+                ("heads", c_int32), ("intermediate", c_int32), ("max_position", c_int32),
+                ("type_vocab", c_int32), ("pooling", c_int32), ("layer_norm_eps", c_float),
+                ("normalize", c_int32)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "hcr_last_error": (c_char_p, []),
+    "hcr_version": (c_char_p, []),
+    "hcr_device_count": (c_int, []),
+    "hcr_index_create": (c_int, [c_int, c_int, c_int, c_int64, POINTER(c_void_p)]),
+    "hcr_index_destroy": (c_int, [c_void_p]),
+    "hcr_index_reset": (c_int, [c_void_p]),
+    "hcr_index_add": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
+    "hcr_index_add_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
+    "hcr_index_set_id_offset": (c_int, [c_void_p, c_int64]),
+    "hcr_index_size": (c_int64, [c_void_p]),
+    "hcr_index_dim": (c_int, [c_void_p]),
+    "hcr_index_dtype": (c_int, [c_void_p]),
+    "hcr_index_get_rows": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_float)]),
+    "hcr_index_set_rowmask": (c_int, [c_void_p, POINTER(c_uint8), c_int64]),
+    "hcr_search": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, c_int, c_float,
+                           POINTER(c_float), POINTER(c_int64)]),
+    "hcr_search_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_double,
+                                  c_void_p, c_void_p, c_void_p]),
+    "hcr_score_all": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, POINTER(c_double)]),
+    "hcr_index_last_stats": (c_int, [c_void_p, POINTER(SearchStats)]),
+    "hcr_index_set_timing": (c_int, [c_void_p, c_int]),
+    "hcr_merge_topk_device": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
+                                      c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libhcrag_hip.so once (raises if it is missing: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libhcrag_hip.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def check(rc: int) -> None:
+    if rc != HCR_OK:
+        msg = lib().hcr_last_error().decode("utf-8", "replace")
+        if rc == HCR_EINVAL:
+            raise ValueError(msg)
+        raise HcrError(rc, msg)
+
+
+def device_count() -> int:
+    return int(lib().hcr_device_count())

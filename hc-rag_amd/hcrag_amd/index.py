@@ -1,0 +1,177 @@
+"""GPU node-embedding index: the MI355X replacement of the reference's embedding matrix +
+cosine/argsort top-k.
+
+``VectorIndex`` wraps one ``hcr_index`` handle (one GPU, one row shard).  Semantics are the
+reference's: sklearn cosine in fp64 over the stored rows, top-k ordered (score desc, row id
+asc), optional ``(s+1)/2`` map and ``>= threshold`` filter (experiments/main.py:831-857,
+experiments/isRelevant.py:197-210).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, c_double, c_float, c_int64, c_uint8, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import (HCR_BF16, HCR_F16, HCR_F32, HCR_SCORE_COSINE, HCR_SCORE_UNIT, SearchStats,
+                   check, lib)
+
+_DTYPES = {"f16": HCR_F16, "float16": HCR_F16, "bf16": HCR_BF16, "bfloat16": HCR_BF16,
+           "f32": HCR_F32, "float32": HCR_F32}
+
+
+def _np_rows(rows):
+    """Host rows -> (contiguous array, hcr dtype).  float64 input is cast to float32."""
+    a = np.asarray(rows)
+    if a.dtype == np.float16:
+        return np.ascontiguousarray(a), HCR_F16
+    if a.dtype == np.uint16:          # raw bf16 bits
+        return np.ascontiguousarray(a), HCR_BF16
+    return np.ascontiguousarray(a, dtype=np.float32), HCR_F32
+
+
+class VectorIndex:
+    """Brute-force cosine top-k index on one MI355X.
+
+    Parameters
+    ----------
+    dim : embedding width (384 MiniLM, 768 bge-base, 1024 bge-large, ...).
+    dtype : storage dtype, "f16" (default), "bf16" or "f32".
+    device : HIP device ordinal.
+    capacity : rows to pre-reserve.
+    """
+
+    def __init__(self, dim: int, dtype: str = "f16", device: int = 0, capacity: int = 0):
+        if dtype not in _DTYPES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        self._h = c_void_p()
+        check(lib().hcr_index_create(int(device), int(dim), _DTYPES[dtype], int(capacity),
+                                     ctypes.byref(self._h)))
+        self.dim = int(dim)
+        self.dtype = dtype
+        self.device = int(device)
+        self.id_offset = 0
+
+    # -- lifecycle ----------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().hcr_index_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- contents -----------------------------------------------------------------------
+    def __len__(self) -> int:
+        return int(lib().hcr_index_size(self._h))
+
+    def add(self, rows, normalize: bool = True) -> None:
+        """Append rows (n x dim, float32/float64/float16, or uint16 bf16 bits)."""
+        a, dt = _np_rows(rows)
+        if a.ndim == 1:
+            a = a.reshape(1, -1)
+        if a.ndim != 2 or a.shape[1] != self.dim:
+            raise ValueError(f"rows must be (n, {self.dim}), got {a.shape}")
+        if a.shape[0] == 0:
+            return
+        check(lib().hcr_index_add(self._h, a.ctypes.data_as(c_void_p), int(a.shape[0]), dt,
+                                  1 if normalize else 0))
+
+    def add_device(self, ptr: int, n: int, rows_dtype: int, normalize: bool = False,
+                   stream: int = 0) -> None:
+        """Append n rows already in HBM (device pointer, e.g. ``tensor.data_ptr()``)."""
+        check(lib().hcr_index_add_device(self._h, c_void_p(ptr), int(n), int(rows_dtype),
+                                         1 if normalize else 0, c_void_p(stream or None)))
+
+    def reset(self) -> None:
+        """Drop all rows (device storage is kept for reuse)."""
+        check(lib().hcr_index_reset(self._h))
+
+    def set_id_offset(self, offset: int) -> None:
+        check(lib().hcr_index_set_id_offset(self._h, int(offset)))
+        self.id_offset = int(offset)
+
+    def get_rows(self, row0: int = 0, n: int | None = None) -> np.ndarray:
+        """Decoded stored rows as float32 (what the index actually ranks)."""
+        if n is None:
+            n = len(self) - row0
+        out = np.empty((n, self.dim), dtype=np.float32)
+        check(lib().hcr_index_get_rows(self._h, int(row0), int(n),
+                                       out.ctypes.data_as(POINTER(c_float))))
+        return out
+
+    def set_rowmask(self, mask) -> None:
+        """Restrict searches to rows with mask != 0 (None clears)."""
+        if mask is None:
+            check(lib().hcr_index_set_rowmask(self._h, None, 0))
+            return
+        m = np.ascontiguousarray(np.asarray(mask, dtype=bool).astype(np.uint8))
+        check(lib().hcr_index_set_rowmask(self._h, m.ctypes.data_as(POINTER(c_uint8)),
+                                          int(m.shape[0])))
+
+    # -- queries ------------------------------------------------------------------------
+    def search(self, queries, k: int, score_mode: int = HCR_SCORE_COSINE,
+               threshold: float = -np.inf):
+        """Top-k per query.  Returns (scores float32 [nq,k], ids int64 [nq,k]); -1 = empty."""
+        q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))
+        if q.shape[1] != self.dim:
+            raise ValueError(
+                f"Incompatible dimension for X and Y matrices: X.shape[1] == {q.shape[1]} "
+                f"while Y.shape[1] == {self.dim}")
+        nq = q.shape[0]
+        s = np.empty((nq, k), dtype=np.float32)
+        i = np.empty((nq, k), dtype=np.int64)
+        check(lib().hcr_search(self._h, q.ctypes.data_as(POINTER(c_float)), nq, int(k),
+                               int(score_mode), float(threshold),
+                               s.ctypes.data_as(POINTER(c_float)),
+                               i.ctypes.data_as(POINTER(c_int64))))
+        return s, i
+
+    def search_device(self, q_ptr: int, nq: int, k: int, out_scores_ptr: int, out_ids_ptr: int,
+                      score_mode: int = HCR_SCORE_COSINE, threshold: float = -np.inf,
+                      stream: int = 0) -> None:
+        """HBM-resident variant: fp32 queries in, fp64 scores / int64 ids out (device ptrs)."""
+        check(lib().hcr_search_device(self._h, c_void_p(q_ptr), int(nq), int(k),
+                                      int(score_mode), float(threshold), c_void_p(out_scores_ptr),
+                                      c_void_p(out_ids_ptr), c_void_p(stream or None)))
+
+    def score_all(self, queries, score_mode: int = HCR_SCORE_COSINE) -> np.ndarray:
+        """Exact fp64 cosine of every (query, row): [nq, len(self)]."""
+        q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))
+        if q.shape[1] != self.dim:
+            raise ValueError("dimension mismatch")
+        out = np.empty((q.shape[0], len(self)), dtype=np.float64)
+        check(lib().hcr_score_all(self._h, q.ctypes.data_as(POINTER(c_float)), q.shape[0],
+                                  int(score_mode), out.ctypes.data_as(POINTER(c_double))))
+        return out
+
+    def last_stats(self) -> dict:
+        st = SearchStats()
+        check(lib().hcr_index_last_stats(self._h, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in SearchStats._fields_}
+
+    def set_timing(self, enable: bool = True) -> None:
+        """HIP-event timing of the fused score kernel (reported by ``last_stats``)."""
+        check(lib().hcr_index_set_timing(self._h, 1 if enable else 0))
+
+
+def merge_topk_device(scores_ptr: int, ids_ptr: int, g: int, nq: int, k: int,
+                      out_scores_ptr: int, out_ids_ptr: int, stream: int = 0) -> None:
+    """Merge g shards' [g][nq][k] exact top-k lists on device."""
+    check(lib().hcr_merge_topk_device(c_void_p(scores_ptr), c_void_p(ids_ptr), int(g), int(nq),
+                                      int(k), c_void_p(out_scores_ptr), c_void_p(out_ids_ptr),
+                                      c_void_p(stream or None)))
+
+
+__all__ = ["VectorIndex", "merge_topk_device", "HCR_SCORE_COSINE", "HCR_SCORE_UNIT",
+           "HCR_F16", "HCR_BF16", "HCR_F32", "_lib"]

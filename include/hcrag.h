@@ -1,0 +1,144 @@
+/*
+ * hcrag.h — C ABI of libhcrag_hip.so, the MI355X-native embedding + vector-retrieval core
+ * for HC-RAG's hot path.  Plain pointers and sizes only; no C++ exceptions
+ * cross this boundary; every call returns an hcr_status (0 = OK, < 0 = error class) and
+ * hcr_last_error() gives a thread-local message.
+ *
+ * The reference has no FFI: its callers bind Python-level interfaces that sit on
+ * third-party CPU engines.  Each entry point below names the reference interface it
+ * replaces (file:line in /root/reference) — the ctypes binding a maintainer adds is in
+ * INTEGRATION.md.
+ *
+ * Ownership / threading:
+ *   - host buffers are borrowed for the duration of the call only; the library owns all
+ *     device memory and its stream; host-pointer calls are synchronous.
+ *   - *_device calls take device pointers and a hipStream_t (as void*) and are
+ *     asynchronous on that stream (inputs already resident in HBM).
+ *   - a handle is not re-entrant; different handles may be used from different threads.
+ */
+#ifndef HCRAG_H_
+#define HCRAG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  HCR_OK = 0,
+  HCR_EINVAL = -1,   /* invalid argument (the reference raises ValueError here) */
+  HCR_EHIP = -2,     /* HIP runtime error */
+  HCR_ERCCL = -3,    /* collective error (reserved; collectives live in the Python host) */
+  HCR_ENOMEM = -4,   /* device allocation failed */
+  HCR_EIO = -5       /* file / format error (encoder weights, vocab) */
+} hcr_status;
+
+typedef enum { HCR_F16 = 0, HCR_BF16 = 1, HCR_F32 = 2 } hcr_dtype;
+
+typedef enum {
+  HCR_SCORE_COSINE = 0,     /* raw cosine: experiments/main.py:841 */
+  HCR_SCORE_UNIT = 1        /* (cos + 1) / 2: experiments/isRelevant.py:208 */
+} hcr_score_mode;
+
+typedef struct hcr_index hcr_index;
+
+/* Last error message of the calling thread ("" if none). */
+const char* hcr_last_error(void);
+/* Library version string. */
+const char* hcr_version(void);
+/* Number of visible HIP devices (0 when no GPU); never fails. */
+int hcr_device_count(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Node-embedding index (brute-force cosine top-k).
+ * Replaces the embedding matrix of experiments/main.py:762 (np.array of the pickled
+ * embeddings) and LlamaIndex SimpleVectorStore's embedding dict (reached from
+ * query_interface.py:200-204, graph_builder.py:161,493-498).
+ * ------------------------------------------------------------------------------------- */
+
+/* Create an empty index on HIP device `device` for `dim`-wide rows stored as `dtype`
+ * (HCR_F16 / HCR_BF16 / HCR_F32).  `capacity_rows` pre-reserves storage (0 = grow). */
+int hcr_index_create(int device, int dim, int dtype, int64_t capacity_rows, hcr_index** out);
+int hcr_index_destroy(hcr_index* index);
+/* Drop all rows and the row mask, keeping device storage for reuse. */
+int hcr_index_reset(hcr_index* index);
+
+/* Append `n` host rows (`rows_dtype`, row-major n x dim).  Row ids are insertion order.
+ * `normalize` = 1 stores each row L2-normalised (computed in fp64) before rounding to the
+ * storage dtype; 0 stores the values as given (rounded).  Cosine is scale-invariant, so
+ * either way the index ranks by sklearn cosine of the STORED (decoded) values.
+ * Replaces DynamicEmbeddingGenerator's list append (experiments/embedding_generator.py:127)
+ * + the matrix build (experiments/main.py:762). */
+int hcr_index_add(hcr_index* index, const void* rows, int64_t n, int rows_dtype, int normalize);
+/* Same from device memory, asynchronous on `stream` (hipStream_t or NULL). */
+int hcr_index_add_device(hcr_index* index, const void* d_rows, int64_t n, int rows_dtype,
+                         int normalize, void* stream);
+
+/* Global id of this index's row 0 (row-sharded indexes: shard offset).  Search results
+ * report id_offset + local row. */
+int hcr_index_set_id_offset(hcr_index* index, int64_t id_offset);
+
+int64_t hcr_index_size(const hcr_index* index);
+int hcr_index_dim(const hcr_index* index);
+int hcr_index_dtype(const hcr_index* index);
+
+/* Copy stored rows [row0, row0+n) back to host as float32 (decoded storage values). */
+int hcr_index_get_rows(const hcr_index* index, int64_t row0, int64_t n, float* out_rows);
+
+/* Restrict searches to rows whose mask byte is non-zero (NULL clears the mask).  `n` must
+ * equal the index size.  Replaces the category filter of experiments/main.py:872-885. */
+int hcr_index_set_rowmask(hcr_index* index, const uint8_t* mask, int64_t n);
+
+/* Batched top-k search: for each of `nq` float32 queries, the k rows of best cosine
+ * (sklearn semantics in fp64 on the stored values; tie rule score desc, id asc), mapped
+ * by `score_mode`, then kept only if score >= `threshold` (pass -INFINITY for none).
+ * Outputs (host, nq x k): scores (float32), ids (int64, -1 = empty slot, score -inf).
+ * Replaces cosine_similarity + np.argsort(...)[::-1][:top_k] + threshold filter of
+ * experiments/main.py:841-849 (and :886-889), and get_top_k_embeddings behind
+ * VectorContextRetriever (query_interface.py:200-204).  k <= 256. */
+int hcr_search(hcr_index* index, const float* queries, int64_t nq, int k, int score_mode,
+               float threshold, float* out_scores, int64_t* out_ids);
+
+/* Device variant: queries (float32, nq x dim), outputs in device memory; fp64 scores so
+ * that row-sharded results merge exactly across GPUs.  Kernels run on `stream`; the call
+ * synchronises that stream once per pass to read the certificate count, so
+ * outputs are final when it returns. */
+int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
+                      int score_mode, double threshold, double* d_out_scores,
+                      int64_t* d_out_ids, void* stream);
+
+/* Exact fp64 cosine of every (query, row) pair, host outputs nq x size (float64).
+ * Replaces the full-score vector of experiments/isRelevant.py:206 (batch_semantic_similarity
+ * returns every node's score, in node order).  Intended for small indexes. */
+int hcr_score_all(hcr_index* index, const float* queries, int64_t nq, int score_mode,
+                  double* out_scores);
+
+/* Statistics of the last search on this handle: candidates kept per query (k'), queries
+ * whose top-k needed a widened candidate set, queries left uncertified after widening. */
+typedef struct {
+  int32_t kprime;
+  int32_t widened_queries;
+  int32_t uncertified_queries;
+  int32_t partitions;
+  int32_t score_launches;     /* score kernel launches timed (timing enabled only) */
+  int32_t workgroups;         /* score kernel grid size of the first pass */
+  double score_kernel_ms;     /* summed HIP-event time of those launches */
+} hcr_search_stats;
+int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
+/* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
+ * is launched on; results appear in hcr_search_stats. */
+int hcr_index_set_timing(hcr_index* index, int enable);
+
+/* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)
+ * into the global top-k (score desc, id asc).  Used after the cross-GPU exchange of
+ * SURVEY.md §8(e).  Asynchronous on `stream`. */
+int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, int64_t nq,
+                          int k, double* d_out_scores, int64_t* d_out_ids, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HCRAG_H_ */

@@ -1,0 +1,267 @@
+"""GPU parity: the HIP top-k path (through the C ABI) vs the CPU oracle / sklearn goldens.
+
+Bar (BASELINE.json north_star): identical top-k index sets and cosine scores within 1e-4.
+The HIP path re-scores its candidates in fp64 and certifies the candidate set, so ids are
+compared EXACTLY and scores to 1e-6 (float32 host API) / 1e-12 (fp64 device API).
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cosine_topk as O
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL_F32 = 1e-6     # float32 host outputs of an fp64 exact score
+SCORE_TOL_F64 = 1e-12    # fp64 device outputs (re-scored in fp64 on the GPU)
+
+
+@pytest.fixture(scope="module")
+def hc():
+    import hcrag_amd
+    if hcrag_amd.device_count() == 0:
+        pytest.fail("GPU test collected but no HIP device visible")
+    return hcrag_amd
+
+
+def _check(got_s, got_i, exp_s, exp_i, tol=SCORE_TOL_F32):
+    np.testing.assert_array_equal(got_i, exp_i)
+    ok = exp_i >= 0
+    np.testing.assert_allclose(got_s[ok], exp_s[ok], rtol=0, atol=tol)
+    assert np.all(np.isneginf(got_s[~ok]))
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(
+    os.path.dirname(__file__), "golden", "cos_*.npz"))))
+def test_golden_fixtures_f16(hc, path):
+    g = np.load(path)
+    E, Q, k = g["E"], g["Q"], int(g["k"])
+    with hc.VectorIndex(E.shape[1], "f16") as ix:
+        ix.add(E, normalize=False)                 # store the fixture's fp16 values exactly
+        np.testing.assert_array_equal(ix.get_rows(), E.astype(np.float32))
+        s, i = ix.search(Q, k)
+        _check(s, i, g["scores"], g["ids"])
+        assert ix.last_stats()["uncertified_queries"] == 0
+
+
+def test_known_answers_gpu(hc, golden_dir):
+    ka = json.load(open(os.path.join(golden_dir, "known_answers.json")))
+    d = ka["dim"]
+    vec = {"ones": np.ones(d), "-ones": -np.ones(d), "random": np.array(ka["random_node"])}
+    vec["e0"] = np.eye(1, d, 0)[0]
+    vec["e1"] = np.eye(1, d, 1)[0]
+    for case in ka["cases"]:
+        got = hc.batch_semantic_similarity(vec[case["query"]], [vec[n] for n in case["nodes"]])
+        assert len(got) == len(case["nodes"])
+        if "tol" in case:
+            for gv, e in zip(got, case["expected"]):
+                assert abs(gv - e) < case["tol"]
+        if "range" in case:
+            lo, hi = case["range"]
+            assert all(lo <= gv <= hi for gv in got)
+            # random node is stored as float32 by the GPU path: 1e-7 vs the fp64 reference
+            np.testing.assert_allclose(got, case["expected"], rtol=0, atol=1e-7)
+    assert hc.batch_semantic_similarity(np.ones(8), []) == []
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16", "f32"])
+@pytest.mark.parametrize("dim", [384, 768, 100])
+def test_random_parity_dtypes(hc, dtype, dim):
+    rng = np.random.default_rng(dim + len(dtype))
+    N, B, k = 5000, 200, 32
+    E = rng.standard_normal((N, dim)).astype(np.float32)
+    Q = rng.standard_normal((B, dim)).astype(np.float32)
+    Q[: B // 2] = E[rng.integers(0, N, B // 2)] + 0.1 * rng.standard_normal((B // 2, dim)).astype(np.float32)
+    with hc.VectorIndex(dim, dtype) as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()                          # decoded stored rows = what is ranked
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, R, k)
+        _check(s, i, es, ei)
+        st = ix.last_stats()
+        assert st["uncertified_queries"] == 0
+
+
+def test_multiblock_queries_and_partitions(hc):
+    rng = np.random.default_rng(7)
+    N, D, B, k = 60000, 768, 300, 32
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), k)
+        _check(s, i, es, ei)
+        st = ix.last_stats()
+        assert st["partitions"] > 1 and st["uncertified_queries"] == 0
+
+
+def test_edge_cases(hc):
+    rng = np.random.default_rng(3)
+    D = 64
+    with hc.VectorIndex(D, "f16") as ix:
+        # empty index -> all slots empty
+        s, i = ix.search(rng.standard_normal((3, D)), 4)
+        assert np.all(i == -1) and np.all(np.isneginf(s))
+        E = rng.standard_normal((10, D)).astype(np.float16)
+        ix.add(E, normalize=False)
+        # k > n: n results then empty slots
+        q = rng.standard_normal((2, D)).astype(np.float32)
+        s, i = ix.search(q, 16)
+        es, ei = O.cosine_topk(q, E.astype(np.float64), 16)
+        _check(s, i, es, ei)
+        assert np.all(i[:, 10:] == -1)
+        # zero query: all cosines 0, ties by row id
+        s, i = ix.search(np.zeros((1, D), np.float32), 5)
+        np.testing.assert_array_equal(i[0], np.arange(5))
+        np.testing.assert_array_equal(s[0], np.zeros(5, np.float32))
+        # nq = 0
+        s, i = ix.search(np.zeros((0, D), np.float32), 3)
+        assert s.shape == (0, 3)
+        # dimension mismatch -> ValueError (sklearn raises ValueError)
+        with pytest.raises(ValueError):
+            ix.search(np.zeros((1, D + 1), np.float32), 3)
+        with pytest.raises(ValueError):
+            ix.search(q, 0)
+
+
+def test_threshold_and_unit_mode(hc):
+    rng = np.random.default_rng(11)
+    D, N = 384, 3000
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    Q = E[:16].astype(np.float32) + 0.3 * rng.standard_normal((16, D)).astype(np.float32)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        for mode, thr in [(0, 0.3), (1, 0.60), (0, -np.inf), (1, 0.9999)]:
+            s, i = ix.search(Q, 10, score_mode=mode, threshold=thr)
+            es, ei = O.cosine_topk(Q, E.astype(np.float64), 10, score_mode=mode, threshold=thr)
+            _check(s, i, es, ei)
+
+
+def test_rowmask_category_filter(hc):
+    rng = np.random.default_rng(5)
+    D, N = 256, 4000
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    Q = rng.standard_normal((20, D)).astype(np.float32)
+    mask = rng.random(N) < 0.2
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        ix.set_rowmask(mask)
+        s, i = ix.search(Q, 8)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), 8, rowmask=mask)
+        _check(s, i, es, ei)
+        ix.set_rowmask(None)
+        s, i = ix.search(Q, 8)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), 8)
+        _check(s, i, es, ei)
+
+
+def test_duplicate_cluster_forces_widening(hc):
+    """300 identical rows tie at the top: the certificate must widen k' and still give the
+    reference's answer (lowest row ids among the tie)."""
+    rng = np.random.default_rng(9)
+    D, N = 128, 2000
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    dup = rng.choice(N, 300, replace=False)
+    E[dup] = E[dup[0]]
+    Q = np.repeat(E[dup[0]].astype(np.float32)[None], 3, axis=0)
+    Q[1] += 0.001 * rng.standard_normal(D).astype(np.float32)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        s, i = ix.search(Q, 32)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), 32)
+        _check(s, i, es, ei)
+        st = ix.last_stats()
+        assert st["widened_queries"] > 0 and st["uncertified_queries"] == 0
+
+
+def test_score_all_matches_oracle(hc):
+    rng = np.random.default_rng(4)
+    E = rng.standard_normal((257, 384)).astype(np.float32)
+    E[5] = 0
+    Q = rng.standard_normal((3, 384)).astype(np.float32)
+    with hc.VectorIndex(384, "f32") as ix:
+        ix.add(E, normalize=False)
+        for mode in (0, 1):
+            got = ix.score_all(Q, score_mode=mode)
+            exp = O.cosine_similarity64(Q, E)
+            if mode:
+                exp = (exp + 1) / 2
+            np.testing.assert_allclose(got, exp, rtol=0, atol=1e-13)
+
+
+def test_device_api_and_shard_merge(hc):
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(21)
+    D, N, B, k, g = 768, 9000, 130, 16, 3
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    es, ei = O.cosine_topk(Q, E.astype(np.float64), k)
+    dev = torch.device("cuda:0")
+    q_t = torch.from_numpy(Q).to(dev)
+    bounds = np.linspace(0, N, g + 1).astype(int)
+    S = torch.empty((g, B, k), dtype=torch.float64, device=dev)
+    I = torch.empty((g, B, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    for j in range(g):
+        with hc.VectorIndex(D, "f16") as ix:
+            ix.add(E[bounds[j]:bounds[j + 1]], normalize=False)
+            ix.set_id_offset(int(bounds[j]))
+            ix.search_device(q_t.data_ptr(), B, k, S[j].data_ptr(), I[j].data_ptr(), stream=stream)
+    out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
+    out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
+    hc.merge_topk_device(S.data_ptr(), I.data_ptr(), g, B, k, out_s.data_ptr(), out_i.data_ptr(),
+                         stream=stream)
+    torch.cuda.synchronize()
+    _check(out_s.cpu().numpy(), out_i.cpu().numpy(), es, ei, tol=SCORE_TOL_F64)
+
+
+def test_embedding_search_dropin(hc):
+    rng = np.random.default_rng(13)
+    M = rng.standard_normal((441, 384))            # config 1 scale (Product*.csv rows)
+    meta = [{"type": "database_table" if r % 3 else "json_table"} for r in range(441)]
+    texts = [f"Record {r}" for r in range(441)]
+    srch = hc.EmbeddingSearch(M, texts, meta, dtype="f32")
+    q = M[17] + 0.05 * rng.standard_normal(384)
+    res = srch.find_similar_content(q, top_k=5, similarity_threshold=0.3)
+    ref = O.find_similar_content(q.astype(np.float32), M.astype(np.float32), 5, 0.3)
+    assert [r["content"] for r in res] == [texts[i] for i, _ in ref]
+    np.testing.assert_allclose([r["similarity_score"] for r in res], [s for _, s in ref], atol=1e-6)
+    cat = srch.search_by_category(q, "json_table", top_k=4)
+    valid = [i for i, m in enumerate(meta) if m["type"] == "json_table"]
+    refc = O.search_by_category(q.astype(np.float32), M.astype(np.float32), valid, 4)
+    assert [r["rank"] for r in cat["results"]] == [x[0] for x in refc]
+    assert [r["content"] for r in cat["results"]] == [texts[x[2]] for x in refc]
+    assert srch.search_by_category(q, "nope")["results"] == []
+
+
+@pytest.mark.slow
+def test_large_planted_recall_and_subset_parity(hc):
+    """2M x 768 fp16: planted queries find their source row first (size-independent
+    property) and a query subset matches the streamed fp64 oracle exactly."""
+    torch = pytest.importorskip("torch")
+    N, D, B, k = 2_000_000, 768, 512, 32
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev).manual_seed(3)
+    E = torch.randn((N, D), generator=gen, device=dev, dtype=torch.float16)
+    src = torch.randint(0, N, (B // 2,), generator=gen, device=dev)
+    Q = torch.randn((B, D), generator=gen, device=dev, dtype=torch.float32)
+    Q[: B // 2] = E[src].float() + 0.05 * torch.randn((B // 2, D), generator=gen, device=dev)
+    with hc.VectorIndex(D, "f16", capacity=N) as ix:
+        ix.add_device(E.data_ptr(), N, hc.HCR_F16, normalize=False)
+        S = torch.empty((B, k), dtype=torch.float64, device=dev)
+        I = torch.empty((B, k), dtype=torch.int64, device=dev)
+        ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(),
+                         stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        st = ix.last_stats()
+        assert st["uncertified_queries"] == 0
+        I = I.cpu().numpy()
+        assert np.array_equal(I[: B // 2, 0], src.cpu().numpy())
+        sub = np.r_[0:4, B // 2:B // 2 + 4]
+        Eh = E.cpu().numpy()
+        es, ei = O.cosine_topk(Q.cpu().numpy()[sub], Eh, k, chunk_rows=1 << 19)
+        _check(S.cpu().numpy()[sub], I[sub], es, ei, tol=SCORE_TOL_F64)
