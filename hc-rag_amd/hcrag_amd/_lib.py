@@ -67,6 +67,40 @@ _SIGS = {
 }
 
 _lib = None
+_runtime = None
+
+
+def _bind_hip_runtime():
+    """One HIP runtime per process.
+
+    PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7, but its libc10_hip
+    NEEDs the file name ``libamdhip64.so``).  If /opt/rocm's runtime were loaded first (by
+    this library) torch would load a second runtime and find no GPU.  So when torch is
+    installed, preload torch's exact runtime files RTLD_GLOBAL: our NEEDED
+    libamdhip64.so.7 then resolves to it by SONAME, and torch's later dlopen of the same
+    file resolves to the same object.  ``HCRAG_HIP_RUNTIME=system`` skips this.
+    """
+    global _runtime
+    if _runtime is not None or os.environ.get("HCRAG_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+    _runtime = "system"
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    tl = os.path.join(os.path.dirname(spec.origin), "lib")
+    hip = os.path.join(tl, "libamdhip64.so")
+    if not os.path.exists(hip):
+        return
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(tl, name)
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    _runtime = hip
+
+
+def runtime_path() -> str:
+    return _runtime or "unloaded"
 
 
 def lib() -> ctypes.CDLL:
@@ -77,6 +111,7 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(
                 f"libhcrag_hip.so not found at {LIB_PATH}; build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+        _bind_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name, None)
