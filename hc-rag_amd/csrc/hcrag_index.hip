@@ -181,7 +181,7 @@ extern "C" int hcr_index_reset(hcr_index* ix) {
 static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows) {
   if (want_rows <= ix->cap) return HCR_OK;
   int64_t ncap = std::max<int64_t>(want_rows, ix->cap + ix->cap / 2);
-  ncap = round_up(std::max<int64_t>(ncap, 128), 128);
+  ncap = round_up(std::max<int64_t>(ncap, 256), 256);   // K2 v2 reads whole 256-row tiles
   const size_t es = dtype_size(ix->dtype);
   DevBuf nrows, nn64, ninv, nmask;
   CHECK(nrows.ensure((size_t)ncap * ix->ld * es));
@@ -373,9 +373,9 @@ static int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 static constexpr int kMaxKprime = 512;
 static constexpr int kMergeMaxKeys = 8192;      // 64 KiB of LDS in merge_partials_kernel
 static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
+static int kV2MinQueries = 384;                 // batch size from which K2 v2 is used
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
-static int cap_for(int kp) { return next_pow2(kp + BR); }
 
 template <typename TS, typename TM, int CAP>
 static void launch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
@@ -399,6 +399,26 @@ static int dispatch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, int
   return HCR_OK;
 }
 
+template <typename TM, int CAP>
+static void launch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
+  hipLaunchKernelGGL((score_topk256_kernel<TM, CAP>), dim3(nqb * P), dim3(NT2), 0, st,
+                     ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / BK, ix->inv32.as<const float>(),
+                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                     ix->w_qhat.as<const TM>(), nqb, P, ntiles, ix->w_buf.as<uint64_t>(),
+                     ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), kp);
+}
+
+template <typename TM>
+static int dispatch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, int cap, hipStream_t st) {
+  switch (cap) {
+    case 512: launch_score256<TM, 512>(ix, nqb, P, ntiles, kp, st); break;
+    case 1024: launch_score256<TM, 1024>(ix, nqb, P, ntiles, kp, st); break;
+    default: return set_err(HCR_EINVAL, "internal: unsupported candidate capacity %d", cap);
+  }
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 template <typename TS>
 static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d_q, int nq, int kp, int k, int mode,
                            double thr, double* out_s, int64_t* out_i, hipStream_t st) {
@@ -415,11 +435,16 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                        double* d_out_s, int64_t* d_out_i, int kp, hipStream_t st, int* n_unc,
                        std::vector<int>* unc_list) {
   const uint64_t* merged_ptr = nullptr;
-  const int nqpad = (int)round_up(nq, BQ);
-  const int nqb = nqpad / BQ;
-  const int ntiles = (int)((ix->n + BR - 1) / BR);
-  const int cap = cap_for(kp);
-  int P = std::max(1, (512 + nqb - 1) / nqb);
+  // kernel choice: v2 (256 x 256 tiles, LDS-DMA) for large batches of 16-bit rows,
+  // v1 (128 x 128 tiles) for small batches and f32 rows.
+  const bool v2 = ix->dtype != HCR_F32 && nq >= kV2MinQueries;
+  const int tq = v2 ? Q2 : BQ, tr = v2 ? R2 : BR;
+  const int nqpad = (int)round_up(nq, tq);
+  const int nqb = nqpad / tq;
+  const int ntiles = (int)((ix->n + tr - 1) / tr);
+  const int cap = next_pow2(kp + tr);
+  const int wg_target = v2 ? 256 : 512;
+  int P = std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
   const bool tm_f16 = ix->dtype == HCR_F16;
@@ -429,7 +454,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_qnorm.ensure((size_t)nqpad * 8));
   CHECK(ix->w_eps.ensure((size_t)nqpad * 8));
   CHECK(ix->w_taug.ensure((size_t)nqpad * 4));
-  CHECK(ix->w_buf.ensure((size_t)nwg * BQ * cap * 8));
+  CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8));
   CHECK(ix->w_part.ensure((size_t)nqpad * P * kp * 8));
   const int G = std::max(2, kMergeMaxKeys / kp);            // partitions merged per block
   const int P2 = (P + G - 1) / G;
@@ -468,7 +493,10 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   HIPC(hipGetLastError());
 
   if (ix->timing) HIPC(hipEventRecord(ix->ev0, st));
-  if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
+  if (v2) {
+    if (ix->dtype == HCR_F16) CHECK((dispatch_score256<_Float16>(ix, nqb, P, ntiles, kp, cap, st)));
+    else CHECK((dispatch_score256<__bf16>(ix, nqb, P, ntiles, kp, cap, st)));
+  } else if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
   else if (ix->dtype == HCR_BF16) CHECK((dispatch_score<__bf16, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));

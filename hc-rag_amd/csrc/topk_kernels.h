@@ -451,6 +451,302 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
 }
 
 // -------------------------------------------------------------------------------------
+// K2 v2 (large batches, 16-bit storage): 256 corpus rows x 256 queries per workgroup.
+//   8 waves = 2 (rows) x 4 (queries); wave tile 128 rows x 64 queries = 8 x 4 accumulators
+//   of MFMA 16x16x32 (128 flop per byte re-read from L2, vs 64 for the 128 x 128 tile).
+//   Operands are staged by LDS-DMA (global_load_lds_dwordx4: no staging VGPRs); the XOR
+//   swizzle is applied to the per-lane SOURCE address so the lane-linear LDS image matches
+//   the conflict-free fragment reads.  Two LDS stages: the DMA for stage s+1 is issued
+//   before the epilogue / MFMAs of stage s and retired by the barrier that ends stage s.
+//   Per-tile inverse norms arrive the same way (3 rotating 1 KiB slots).
+//   Requires: rows / inv_norm allocated to a multiple of 256 rows, qhat to nqb*256 rows.
+// -------------------------------------------------------------------------------------
+constexpr int R2 = 256, Q2 = 256, NT2 = 512;
+constexpr int A2_BYTES = R2 * BK * 2, B2_BYTES = Q2 * BK * 2;
+constexpr int STAGE2 = A2_BYTES + B2_BYTES;                     // 64 KiB
+constexpr int L2_INV = 2 * STAGE2;                              // 3 x 1 KiB inverse norms
+constexpr int L2_MSK = L2_INV + 3 * R2 * 4;                     // 3 x 8 row-mask words
+constexpr int L2_TAU = L2_MSK + 3 * 64;                         // u64 tau_key[256]
+constexpr int L2_CNT = L2_TAU + Q2 * 8;                         // int cnt[256]
+constexpr int L2_FLAG = L2_CNT + Q2 * 4;                        // int flag[2] (tile parity)
+constexpr int L2_TOTAL = L2_FLAG + 16;
+
+// LDS reads the compiler does not see: hipcc would otherwise wait vmcnt(0) for the
+// in-flight LDS-DMA of the next stage before them (a conservative alias assumption).
+__device__ __forceinline__ float4 lds_read_f4_now(const char* p) {
+  float4 v;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint32_t lds_read_u32_now(const char* p) {
+  uint32_t v;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
+                                   (void __attribute__((address_space(3)))*)lds_dst, 16, 0, 0);
+}
+
+template <typename TM, int CAP>
+__global__ void __launch_bounds__(NT2, 2)
+score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
+                     const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
+                     const TM* __restrict__ qhat, int nqb, int P, int ntiles,
+                     uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
+                     uint64_t* __restrict__ partials, int kp) {
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  __shared__ __attribute__((aligned(16))) char lds[L2_TOTAL];
+  uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L2_TAU);
+  int* cnt = reinterpret_cast<int*>(lds + L2_CNT);
+  int* flag = reinterpret_cast<int*>(lds + L2_FLAG);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int qb = g % nqb, p = g / nqb;
+  const int t0 = (int)((int64_t)p * ntiles / P);
+  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
+  const int qbase = qb * Q2;
+  uint64_t* wbuf = buf + (size_t)b * Q2 * CAP;
+
+  for (int i = tid; i < Q2; i += NT2) { tau_key[i] = 0ull; cnt[i] = 0; }
+  if (tid == 0) { flag[0] = 0; flag[1] = 0; }
+
+  if (t0 >= t1) {
+    for (int i = tid; i < Q2 * kp; i += NT2) {
+      const int ql = i / kp, j = i - ql * kp;
+      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
+    }
+    return;
+  }
+
+  // LDS-DMA (buffer_load ... lds): one 32-bit voffset per lane; the 8-row group and the K
+  // offset go in the scalar soffset, the tile base in the buffer descriptor.  Wave w issues
+  // groups g = 4w + i (i = 0..3) of 8 rows; lane l -> row 8g + (l >> 3), logical chunk
+  // (l & 7) ^ (l >> 3) (the XOR of the fragment reads, applied at the source).
+  const int lrow = lane >> 3;
+  const int ldb = ld * 2;                                      // row pitch in bytes
+  const int voff = lrow * ldb + (((lane & 7) ^ lrow) << 4);
+  const char* rows_b = reinterpret_cast<const char*>(rows);
+  auto uniform_ptr = [](const void* p) -> void* {
+    const uint64_t v = (uint64_t)p;
+    return (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                   (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v));
+  };
+  const char* q_b = reinterpret_cast<const char*>(qhat) + (size_t)qbase * ldb;
+  const __amdgpu_buffer_rsrc_t q_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(q_b), (short)0, Q2 * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t inv_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(inv_norm), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t msk_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(mask), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int grp_off = wave * 4 * 8 * ldb;
+
+  auto issue_stage = [&](int tile_, int ks_, int stg_) {
+    // descriptor inputs made provably wave-uniform (else hipcc waterfalls every load)
+    const int tile = __builtin_amdgcn_readfirstlane(tile_);
+    const int ks = __builtin_amdgcn_readfirstlane(ks_);
+    const int stg = __builtin_amdgcn_readfirstlane(stg_);
+    char* sa = lds + stg * STAGE2;
+    const uint64_t abase = (uint64_t)(rows_b + (size_t)tile * R2 * ldb);
+    const uint64_t abu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(abase >> 32)) << 32) |
+                         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)abase);
+    const __amdgpu_buffer_rsrc_t a_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)abu, (short)0, R2 * ldb, 0x00020000);
+    const int kofs = ks * (BK * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int so = grp_off + i * 8 * ldb + kofs;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          a_rsrc, (__attribute__((address_space(3))) void*)(sa + (wave * 4 + i) * 1024), 16,
+          voff, so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          q_rsrc,
+          (__attribute__((address_space(3))) void*)(sa + A2_BYTES + (wave * 4 + i) * 1024), 16,
+          voff, so, 0, 0);
+    }
+    if (ks == 0 && wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          inv_rsrc, (__attribute__((address_space(3))) void*)(lds + L2_INV + (tile % 3) * (R2 * 4)),
+          16, lane * 16, tile * (R2 * 4), 0, 0);
+    if (ks == 0 && wave == 1 && mask) {
+      if (lane < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            msk_rsrc, (__attribute__((address_space(3))) void*)(lds + L2_MSK + (tile % 3) * 64),
+            4, lane * 4, tile * 32, 0, 0);
+    }
+  };
+
+  // fragment read offsets
+  const int fr = lane & 15;
+  const int c0 = (lane >> 4) ^ (lane & 7);
+  const int offA0 = (wm * 128 + fr) * 128 + (c0 << 4);
+  const int offA1 = (wm * 128 + fr) * 128 + ((c0 ^ 4) << 4);
+  const int offB0 = A2_BYTES + (wn * 64 + fr) * 128 + (c0 << 4);
+  const int offB1 = A2_BYTES + (wn * 64 + fr) * 128 + ((c0 ^ 4) << 4);
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  uint32_t tg[4] = {0u, 0u, 0u, 0u};
+  const int nsteps = (t1 - t0) * ksteps;
+
+  issue_stage(t0, 0, 0);
+  __syncthreads();
+
+  int tile = t0, ks = 0;
+  int ep_tile = -1;                      // tile whose epilogue is pending
+  for (int s = 0; s <= nsteps; ++s) {
+    // 1) DMA of the next stage (its buffer was last read in step s-1, before its barrier)
+    int ntile = tile, nks = ks + 1;
+    if (nks == ksteps) { nks = 0; ++ntile; }
+    if (s + 1 < nsteps) issue_stage(ntile, nks, (s + 1) & 1);
+
+    // 2) epilogue of the tile finished by step s-1 (accumulators complete)
+    if (ep_tile >= 0) {
+      // flag[t & 1] is set by epilogue t and consumed (then cleared) at epilogue t + 1,
+      // so a clear never races with the sets of the epilogue that follows it.
+      int* prev_flag = flag + ((ep_tile + 1) & 1);
+      if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
+        for (int ql = wave; ql < Q2; ql += NT2 / 64) {
+          if (cnt[ql] > CAP - R2)
+            compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+                               tau_g + qbase + ql, kp, lane, nullptr);
+        }
+        __syncthreads();
+        if (tid == 0) *prev_flag = 0;
+      }
+      int* cur_flag = flag + (ep_tile & 1);
+      // per-lane addresses are derived from an opaque copy of the lane id so the compiler
+      // recomputes them here instead of hoisting them (and spilling) across the main loop
+      int le;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
+      const int lr = le & 15, lq = le >> 4;
+      const int64_t row0 = (int64_t)ep_tile * R2;
+      const float* invl = reinterpret_cast<const float*>(lds + L2_INV + (ep_tile % 3) * (R2 * 4));
+      const char* mskl = lds + L2_MSK + (ep_tile % 3) * 64;
+      float thr[4];
+      uint64_t tk[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int ql = wn * 64 + n * 16 + lr;
+        tk[n] = tau_key[ql];
+        const float ls = tk[n] ? key_score(tk[n]) : -INFINITY;
+        thr[n] = fmaxf(ls, unord32(tg[n]));
+      }
+      // inverse norm (NaN for rows past the end / masked out) of this lane's row r of m-tile m
+      auto inv4 = [&](int m, float (&iv)[4]) {
+        const int rl = wm * 128 + m * 16 + lq * 4;
+        const float4 v = lds_read_f4_now(reinterpret_cast<const char*>(invl + rl));
+        uint32_t mword = 0xFFFFFFFFu;
+        if (mask) mword = lds_read_u32_now(mskl + (rl >> 5) * 4);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (row0 + rl + r < n_rows) && ((mword >> ((rl + r) & 31)) & 1u);
+          iv[r] = ok ? vv[r] : __builtin_nanf("");
+        }
+      };
+      float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        float iv[4];
+        inv4(m, iv);
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r] * iv[r]);
+      }
+      bool hit[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) hit[n] = mx[n] >= thr[n];
+      if (__any(hit[0] | hit[1] | hit[2] | hit[3])) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          float iv[4];
+          inv4(m, iv);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            if (hit[n]) {
+              const int ql = wn * 64 + n * 16 + lr;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float sc = acc[m][n][r] * iv[r];
+                if (sc >= thr[n]) {
+                  const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
+                  const uint64_t key = make_key(sc, rowl);
+                  if (key > tk[n]) {
+                    const int pos = atomicAdd(&cnt[ql], 1);
+                    wbuf[(size_t)ql * CAP + pos] = key;
+                    if (pos + 1 > CAP - R2) *cur_flag = 1;
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      ep_tile = -1;
+    }
+    if (s == nsteps) break;
+
+    // 3) MFMAs of step s
+    const bool last_k = (ks == ksteps - 1);
+    if (last_k) {
+      int lt;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(lt) : "v"(lane));
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        tg[n] = __hip_atomic_load(tau_g + qbase + wn * 64 + n * 16 + (lt & 15), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+    {
+      const char* st = lds + (s & 1) * STAGE2;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int oa = kk ? offA1 : offA0;
+        const int ob = kk ? offB1 : offB0;
+        V bq[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(st + ob + n * 16 * 128);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const V a = *reinterpret_cast<const V*>(st + oa + m * 16 * 128);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(a, bq[n], acc[m][n]);
+        }
+      }
+    }
+    __syncthreads();                     // retires the DMA of stage s+1 (vmcnt(0) + barrier)
+    if (last_k) ep_tile = tile;
+    tile = ntile;
+    ks = nks;
+  }
+
+  // final: every query's best kp keys -> partials[q][p][0..kp)
+  for (int ql = wave; ql < Q2; ql += NT2 / 64) {
+    compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
+                       lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // K3: merge the P partition lists of one query into its global top-k' (sorted desc).
 // -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)

@@ -265,3 +265,60 @@ def test_large_planted_recall_and_subset_parity(hc):
         Eh = E.cpu().numpy()
         es, ei = O.cosine_topk(Q.cpu().numpy()[sub], Eh, k, chunk_rows=1 << 19)
         _check(S.cpu().numpy()[sub], I[sub], es, ei, tol=SCORE_TOL_F64)
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+@pytest.mark.parametrize("B", [1, 130, 384, 700])
+def test_batch_sizes_both_kernels(hc, dtype, B):
+    """B < 384 runs the 128x128 kernel, B >= 384 the 256x256 LDS-DMA kernel."""
+    rng = np.random.default_rng(B)
+    N, D, k = 20000, 384, 10
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[: B // 2] = E[rng.integers(0, N, B // 2)] + 0.2 * rng.standard_normal((B // 2, D)).astype(np.float32)
+    with hc.VectorIndex(D, dtype) as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, R, k)
+        _check(s, i, es, ei)
+        assert ix.last_stats()["uncertified_queries"] == 0
+
+
+def test_large_batch_mask_and_widening(hc):
+    """256x256 kernel: row mask + a duplicate cluster that forces k' widening."""
+    rng = np.random.default_rng(17)
+    N, D, B, k = 30000, 256, 512, 32
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    dup = rng.choice(N, 200, replace=False)
+    E[dup] = E[dup[0]]
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[:8] = E[dup[0]].astype(np.float32)
+    mask = rng.random(N) < 0.5
+    mask[dup] = True
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), k)
+        _check(s, i, es, ei)
+        st = ix.last_stats()
+        assert st["widened_queries"] > 0 and st["uncertified_queries"] == 0
+        ix.set_rowmask(mask)
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, E.astype(np.float64), k, rowmask=mask)
+        _check(s, i, es, ei)
+
+
+def test_ragged_tail_rows(hc):
+    """Corpus sizes that end mid-tile (256 and 128 row tiles) and tiny corpora."""
+    rng = np.random.default_rng(23)
+    D = 192
+    for N in (1, 5, 255, 257, 1000, 4097):
+        E = rng.standard_normal((N, D)).astype(np.float16)
+        Q = rng.standard_normal((400, D)).astype(np.float32)
+        with hc.VectorIndex(D, "f16") as ix:
+            ix.add(E, normalize=False)
+            for qs in (Q[:3], Q):
+                s, i = ix.search(qs, 7)
+                es, ei = O.cosine_topk(qs, E.astype(np.float64), 7)
+                _check(s, i, es, ei)
