@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -103,6 +104,7 @@ struct hcr_index {
 };
 
 static size_t dtype_size(int dt) { return dt == HCR_F32 ? 4 : 2; }
+static constexpr int64_t kSlackRows = 512;
 static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows);
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -174,22 +176,26 @@ extern "C" int hcr_index_reset(hcr_index* ix) {
   ix->has_mask = false;
   ix->rho_dirty = true;
   HIPC(hipMemset(ix->rho.p, 0, 16));
-  if (ix->cap > 0) HIPC(hipMemset(ix->maskbits.p, 0xFF, (size_t)(ix->cap / 32) * 4));
+  if (ix->cap > 0) HIPC(hipMemset(ix->maskbits.p, 0xFF, (size_t)((ix->cap + kSlackRows) / 32) * 4));
   return HCR_OK;
 }
 
 static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows) {
   if (want_rows <= ix->cap) return HCR_OK;
   int64_t ncap = std::max<int64_t>(want_rows, ix->cap + ix->cap / 2);
-  ncap = round_up(std::max<int64_t>(ncap, 256), 256);   // K2 v2 reads whole 256-row tiles
+  ncap = round_up(std::max<int64_t>(ncap, 256), 256);
+  // kSlackRows past the capacity: the score kernels read whole tiles (and DMA whole 1 KiB
+  // inverse-norm slots), so every allocation covers the last tile plus slack.
+  const int64_t arows = ncap + kSlackRows;
   const size_t es = dtype_size(ix->dtype);
   DevBuf nrows, nn64, ninv, nmask;
-  CHECK(nrows.ensure((size_t)ncap * ix->ld * es));
-  CHECK(nn64.ensure((size_t)ncap * 8));
-  CHECK(ninv.ensure((size_t)ncap * 4));
-  CHECK(nmask.ensure((size_t)(ncap / 32) * 4));
-  HIPC(hipMemsetAsync(ninv.p, 0, (size_t)ncap * 4, ix->stream));
-  HIPC(hipMemsetAsync(nmask.p, 0xFF, (size_t)(ncap / 32) * 4, ix->stream));
+  CHECK(nrows.ensure((size_t)arows * ix->ld * es));
+  CHECK(nn64.ensure((size_t)arows * 8));
+  CHECK(ninv.ensure((size_t)arows * 4));
+  CHECK(nmask.ensure((size_t)(arows / 32) * 4));
+  HIPC(hipMemsetAsync(nrows.p, 0, (size_t)arows * ix->ld * es, ix->stream));
+  HIPC(hipMemsetAsync(ninv.p, 0, (size_t)arows * 4, ix->stream));
+  HIPC(hipMemsetAsync(nmask.p, 0xFF, (size_t)(arows / 32) * 4, ix->stream));
   if (ix->n > 0) {
     HIPC(hipMemcpyAsync(nrows.p, ix->rows.p, (size_t)ix->n * ix->ld * es, hipMemcpyDeviceToDevice, ix->stream));
     HIPC(hipMemcpyAsync(nn64.p, ix->norm64.p, (size_t)ix->n * 8, hipMemcpyDeviceToDevice, ix->stream));
@@ -340,7 +346,7 @@ extern "C" int hcr_index_set_rowmask(hcr_index* ix, const uint8_t* mask, int64_t
   if (!mask) { ix->has_mask = false; return HCR_OK; }
   if (n != ix->n) return set_err(HCR_EINVAL, "mask length %lld != index size %lld", (long long)n, (long long)ix->n);
   if (ix->cap == 0) { ix->has_mask = false; return HCR_OK; }
-  std::vector<uint32_t> bits((size_t)(ix->cap / 32), 0u);
+  std::vector<uint32_t> bits((size_t)((ix->cap + kSlackRows) / 32), 0u);
   for (int64_t i = 0; i < n; ++i)
     if (mask[i]) bits[(size_t)(i >> 5)] |= 1u << (i & 31);
   HIPC(hipMemcpyAsync(ix->maskbits.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ix->stream));
@@ -401,7 +407,7 @@ static int dispatch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, int
 
 template <typename TM, int CAP>
 static void launch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk256_kernel<TM, CAP>), dim3(nqb * P), dim3(NT2), 0, st,
+  hipLaunchKernelGGL((score_topk224_kernel<TM, CAP>), dim3(nqb * P), dim3(NT2), 0, st,
                      ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / BK, ix->inv32.as<const float>(),
                      ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                      ix->w_qhat.as<const TM>(), nqb, P, ntiles, ix->w_buf.as<uint64_t>(),
@@ -437,7 +443,8 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const uint64_t* merged_ptr = nullptr;
   // kernel choice: v2 (256 x 256 tiles, LDS-DMA) for large batches of 16-bit rows,
   // v1 (128 x 128 tiles) for small batches and f32 rows.
-  const bool v2 = ix->dtype != HCR_F32 && nq >= kV2MinQueries;
+  static const bool v2_disabled = getenv("HCRAG_DISABLE_V2") != nullptr;
+  const bool v2 = !v2_disabled && ix->dtype != HCR_F32 && nq >= kV2MinQueries;
   const int tq = v2 ? Q2 : BQ, tr = v2 ? R2 : BR;
   const int nqpad = (int)round_up(nq, tq);
   const int nqb = nqpad / tq;

@@ -451,25 +451,29 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
 }
 
 // -------------------------------------------------------------------------------------
-// K2 v2 (large batches, 16-bit storage): 256 corpus rows x 256 queries per workgroup.
-//   8 waves = 2 (rows) x 4 (queries); wave tile 128 rows x 64 queries = 8 x 4 accumulators
-//   of MFMA 16x16x32 (128 flop per byte re-read from L2, vs 64 for the 128 x 128 tile).
-//   Operands are staged by LDS-DMA (global_load_lds_dwordx4: no staging VGPRs); the XOR
-//   swizzle is applied to the per-lane SOURCE address so the lane-linear LDS image matches
-//   the conflict-free fragment reads.  Two LDS stages: the DMA for stage s+1 is issued
-//   before the epilogue / MFMAs of stage s and retired by the barrier that ends stage s.
-//   Per-tile inverse norms arrive the same way (3 rotating 1 KiB slots).
-//   Requires: rows / inv_norm allocated to a multiple of 256 rows, qhat to nqb*256 rows.
+// K2 v2 (large batches, 16-bit storage): 224 corpus rows x 256 queries per workgroup.
+//   8 waves = 2 (rows) x 4 (queries); wave tile 112 rows x 64 queries = 7 x 4 accumulators
+//   of MFMA 16x16x32 (119 flop per byte re-read from L2, vs 64 for the 128 x 128 tile).
+//   Operands are staged by LDS-DMA (buffer_load ... lds: no staging VGPRs); the XOR swizzle
+//   is applied to the per-lane SOURCE offset so the lane-linear LDS image matches the
+//   conflict-free fragment reads.  Two LDS stages: the DMA for stage s+1 is issued before
+//   the epilogue / MFMAs of stage s and retired by the barrier that ends stage s.  Per-tile
+//   inverse norms and row-mask words arrive the same way (3 rotating slots).
+//   224 rows (not 256) keeps the whole LDS image, and every DMA target, below 128 KiB.
+//   Requires: rows / inv_norm / mask allocated with >= 256 rows of slack past the last
+//   tile, qhat allocated to nqb*256 rows (padding rows zero).
 // -------------------------------------------------------------------------------------
-constexpr int R2 = 256, Q2 = 256, NT2 = 512;
-constexpr int A2_BYTES = R2 * BK * 2, B2_BYTES = Q2 * BK * 2;
-constexpr int STAGE2 = A2_BYTES + B2_BYTES;                     // 64 KiB
+constexpr int R2 = 224, Q2 = 256, NT2 = 512;
+constexpr int MT2 = R2 / 32;                                    // m-tiles per wave (7)
+constexpr int A2_BYTES = R2 * BK * 2, B2_BYTES = Q2 * BK * 2;   // 28 KiB + 32 KiB
+constexpr int STAGE2 = A2_BYTES + B2_BYTES;
 constexpr int L2_INV = 2 * STAGE2;                              // 3 x 1 KiB inverse norms
-constexpr int L2_MSK = L2_INV + 3 * R2 * 4;                     // 3 x 8 row-mask words
+constexpr int L2_MSK = L2_INV + 3 * 1024;                       // 3 x 8 row-mask words
 constexpr int L2_TAU = L2_MSK + 3 * 64;                         // u64 tau_key[256]
 constexpr int L2_CNT = L2_TAU + Q2 * 8;                         // int cnt[256]
 constexpr int L2_FLAG = L2_CNT + Q2 * 4;                        // int flag[2] (tile parity)
 constexpr int L2_TOTAL = L2_FLAG + 16;
+static_assert(L2_TOTAL <= 128 * 1024, "v2 LDS image must stay below 128 KiB");
 
 // LDS reads the compiler does not see: hipcc would otherwise wait vmcnt(0) for the
 // in-flight LDS-DMA of the next stage before them (a conservative alias assumption).
@@ -485,15 +489,19 @@ __device__ __forceinline__ uint32_t lds_read_u32_now(const char* p) {
   asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
   return v;
 }
-
-__device__ __forceinline__ void glds16(const void* gsrc, char* lds_dst) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)gsrc,
-                                   (void __attribute__((address_space(3)))*)lds_dst, 16, 0, 0);
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_dst, 16,
+                                           voff, soff, 0, 0);
+}
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)p;
+  return (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+                 (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v));
 }
 
 template <typename TM, int CAP>
 __global__ void __launch_bounds__(NT2, 2)
-score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
+score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
@@ -529,74 +537,56 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     return;
   }
 
-  // LDS-DMA (buffer_load ... lds): one 32-bit voffset per lane; the 8-row group and the K
-  // offset go in the scalar soffset, the tile base in the buffer descriptor.  Wave w issues
-  // groups g = 4w + i (i = 0..3) of 8 rows; lane l -> row 8g + (l >> 3), logical chunk
-  // (l & 7) ^ (l >> 3) (the XOR of the fragment reads, applied at the source).
+  // LDS-DMA: one 32-bit voffset per lane (row inside an 8-row group + swizzled chunk); the
+  // group and K offsets go in the scalar soffset, the tile base in the descriptor.
   const int lrow = lane >> 3;
   const int ldb = ld * 2;                                      // row pitch in bytes
   const int voff = lrow * ldb + (((lane & 7) ^ lrow) << 4);
   const char* rows_b = reinterpret_cast<const char*>(rows);
-  auto uniform_ptr = [](const void* p) -> void* {
-    const uint64_t v = (uint64_t)p;
-    return (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-                   (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v));
-  };
-  const char* q_b = reinterpret_cast<const char*>(qhat) + (size_t)qbase * ldb;
-  const __amdgpu_buffer_rsrc_t q_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(q_b), (short)0, Q2 * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t q_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(qhat) + (size_t)qbase * ldb), (short)0, Q2 * ldb,
+      0x00020000);
   const __amdgpu_buffer_rsrc_t inv_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(inv_norm), (short)0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t msk_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(mask), (short)0, 0x7FFFFFFF, 0x00020000);
-  const int grp_off = wave * 4 * 8 * ldb;
 
   auto issue_stage = [&](int tile_, int ks_, int stg_) {
-    // descriptor inputs made provably wave-uniform (else hipcc waterfalls every load)
-    const int tile = __builtin_amdgcn_readfirstlane(tile_);
-    const int ks = __builtin_amdgcn_readfirstlane(ks_);
+    const int tile = __builtin_amdgcn_readfirstlane(tile_);   // provably uniform descriptor
+    const int ks = __builtin_amdgcn_readfirstlane(ks_);       // inputs: no waterfall loops
     const int stg = __builtin_amdgcn_readfirstlane(stg_);
     char* sa = lds + stg * STAGE2;
-    const uint64_t abase = (uint64_t)(rows_b + (size_t)tile * R2 * ldb);
-    const uint64_t abu = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(abase >> 32)) << 32) |
-                         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)abase);
-    const __amdgpu_buffer_rsrc_t a_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)abu, (short)0, R2 * ldb, 0x00020000);
+    const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        uniform_ptr(rows_b + (size_t)tile * R2 * ldb), (short)0, 256 * ldb, 0x00020000);
     const int kofs = ks * (BK * 2);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int so = grp_off + i * 8 * ldb + kofs;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          a_rsrc, (__attribute__((address_space(3))) void*)(sa + (wave * 4 + i) * 1024), 16,
-          voff, so, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          q_rsrc,
-          (__attribute__((address_space(3))) void*)(sa + A2_BYTES + (wave * 4 + i) * 1024), 16,
-          voff, so, 0, 0);
+      const int grp = wave * 4 + i;                            // 8-row group
+      const int so = grp * 8 * ldb + kofs;
+      if (grp < R2 / 8) dma16(a_rsrc, sa + grp * 1024, voff, so);
+      dma16(q_rsrc, sa + A2_BYTES + grp * 1024, voff, so);
     }
-    if (ks == 0 && wave == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          inv_rsrc, (__attribute__((address_space(3))) void*)(lds + L2_INV + (tile % 3) * (R2 * 4)),
-          16, lane * 16, tile * (R2 * 4), 0, 0);
+    if (ks == 0 && wave == 0)   // 256 floats (224 used) of this tile's inverse norms
+      dma16(inv_rsrc, lds + L2_INV + (tile % 3) * 1024, lane * 16, tile * (R2 * 4));
     if (ks == 0 && wave == 1 && mask) {
       if (lane < 8)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             msk_rsrc, (__attribute__((address_space(3))) void*)(lds + L2_MSK + (tile % 3) * 64),
-            4, lane * 4, tile * 32, 0, 0);
+            4, lane * 4, tile * (R2 / 8), 0, 0);
     }
   };
 
   // fragment read offsets
   const int fr = lane & 15;
   const int c0 = (lane >> 4) ^ (lane & 7);
-  const int offA0 = (wm * 128 + fr) * 128 + (c0 << 4);
-  const int offA1 = (wm * 128 + fr) * 128 + ((c0 ^ 4) << 4);
+  const int offA0 = (wm * (R2 / 2) + fr) * 128 + (c0 << 4);
+  const int offA1 = (wm * (R2 / 2) + fr) * 128 + ((c0 ^ 4) << 4);
   const int offB0 = A2_BYTES + (wn * 64 + fr) * 128 + (c0 << 4);
   const int offB1 = A2_BYTES + (wn * 64 + fr) * 128 + ((c0 ^ 4) << 4);
 
-  floatx4 acc[8][4];
+  floatx4 acc[MT2][4];
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+  for (int m = 0; m < MT2; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
@@ -635,7 +625,7 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
       const int lr = le & 15, lq = le >> 4;
       const int64_t row0 = (int64_t)ep_tile * R2;
-      const float* invl = reinterpret_cast<const float*>(lds + L2_INV + (ep_tile % 3) * (R2 * 4));
+      const char* invl = lds + L2_INV + (ep_tile % 3) * 1024;
       const char* mskl = lds + L2_MSK + (ep_tile % 3) * 64;
       float thr[4];
       uint64_t tk[4];
@@ -646,10 +636,10 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         const float ls = tk[n] ? key_score(tk[n]) : -INFINITY;
         thr[n] = fmaxf(ls, unord32(tg[n]));
       }
-      // inverse norm (NaN for rows past the end / masked out) of this lane's row r of m-tile m
+      // inverse norm (NaN for rows past the end / masked out) of this lane's rows in m-tile m
       auto inv4 = [&](int m, float (&iv)[4]) {
-        const int rl = wm * 128 + m * 16 + lq * 4;
-        const float4 v = lds_read_f4_now(reinterpret_cast<const char*>(invl + rl));
+        const int rl = wm * (R2 / 2) + m * 16 + lq * 4;        // row inside the tile
+        const float4 v = lds_read_f4_now(invl + rl * 4);
         uint32_t mword = 0xFFFFFFFFu;
         if (mask) mword = lds_read_u32_now(mskl + (rl >> 5) * 4);
         const float vv[4] = {v.x, v.y, v.z, v.w};
@@ -661,7 +651,7 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       };
       float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
+      for (int m = 0; m < MT2; ++m) {
         float iv[4];
         inv4(m, iv);
 #pragma unroll
@@ -674,7 +664,7 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       for (int n = 0; n < 4; ++n) hit[n] = mx[n] >= thr[n];
       if (__any(hit[0] | hit[1] | hit[2] | hit[3])) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
+        for (int m = 0; m < MT2; ++m) {
           float iv[4];
           inv4(m, iv);
 #pragma unroll
@@ -685,7 +675,7 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
               for (int r = 0; r < 4; ++r) {
                 const float sc = acc[m][n][r] * iv[r];
                 if (sc >= thr[n]) {
-                  const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
+                  const uint32_t rowl = (uint32_t)(row0 + wm * (R2 / 2) + m * 16 + lq * 4 + r);
                   const uint64_t key = make_key(sc, rowl);
                   if (key > tk[n]) {
                     const int pos = atomicAdd(&cnt[ql], 1);
@@ -699,7 +689,7 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         }
       }
 #pragma unroll
-      for (int m = 0; m < 8; ++m)
+      for (int m = 0; m < MT2; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       ep_tile = -1;
@@ -726,10 +716,10 @@ score_topk256_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
 #pragma unroll
         for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(st + ob + n * 16 * 128);
 #pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const V a = *reinterpret_cast<const V*>(st + oa + m * 16 * 128);
+        for (int m = 0; m < MT2; ++m) {
+          const V av = *reinterpret_cast<const V*>(st + oa + m * 16 * 128);
 #pragma unroll
-          for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(a, bq[n], acc[m][n]);
+          for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(av, bq[n], acc[m][n]);
         }
       }
     }

@@ -251,7 +251,8 @@ def test_large_planted_recall_and_subset_parity(hc):
     Q = torch.randn((B, D), generator=gen, device=dev, dtype=torch.float32)
     Q[: B // 2] = E[src].float() + 0.05 * torch.randn((B // 2, D), generator=gen, device=dev)
     with hc.VectorIndex(D, "f16", capacity=N) as ix:
-        ix.add_device(E.data_ptr(), N, hc.HCR_F16, normalize=False)
+        ix.add_device(E.data_ptr(), N, hc.HCR_F16, normalize=False,
+                      stream=torch.cuda.current_stream().cuda_stream)
         S = torch.empty((B, k), dtype=torch.float64, device=dev)
         I = torch.empty((B, k), dtype=torch.int64, device=dev)
         ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(),
