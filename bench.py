@@ -117,7 +117,8 @@ def main():
 
     import hcrag_amd as hc
     N, D, B, k = a.rows, a.dim, a.batch, a.k
-    r0, r1 = rank * N // world, (rank + 1) * N // world
+    from hcrag_amd.distributed import shard_range
+    r0, r1 = shard_range(N, rank, world)
     nloc = r1 - r0
     ix = hc.VectorIndex(D, a.dtype, device=local, capacity=nloc)
     ix.set_id_offset(r0)
@@ -134,29 +135,11 @@ def main():
 
     Q, src = make_queries(rows_fn, B, D, dev, rank, nloc, r0)
     nq = world * B
-    Qall = torch.empty((nq, D), dtype=torch.float32, device=dev)
-    S = torch.empty((nq, k), dtype=torch.float64, device=dev)
-    I = torch.empty((nq, k), dtype=torch.int64, device=dev)
-    Sr = torch.empty((world, B, k), dtype=torch.float64, device=dev)
-    Ir = torch.empty((world, B, k), dtype=torch.int64, device=dev)
-    Out_s = torch.empty((B, k), dtype=torch.float64, device=dev)
-    Out_i = torch.empty((B, k), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream().cuda_stream
+    from hcrag_amd.distributed import ShardedSearch, hip_local_search, hip_merge
+    searcher = ShardedSearch(hip_local_search(ix, k), hip_merge(k), k)
 
     def step():
-        if world > 1:
-            dist.all_gather_into_tensor(Qall, Q)
-            q_ptr = Qall.data_ptr()
-        else:
-            q_ptr = Q.data_ptr()
-        ix.search_device(q_ptr, nq, k, S.data_ptr(), I.data_ptr(), stream=stream)
-        if world > 1:
-            dist.all_to_all_single(Sr.view(world * B, k), S)
-            dist.all_to_all_single(Ir.view(world * B, k), I)
-            hc.merge_topk_device(Sr.data_ptr(), Ir.data_ptr(), world, B, k, Out_s.data_ptr(),
-                                 Out_i.data_ptr(), stream=stream)
-            return Out_i
-        return I
+        return searcher.search(Q)[1]
 
     for _ in range(a.warmup):
         step()
@@ -222,6 +205,7 @@ def main():
             Qs = torch.randn((bsz, D), device=dev)
             Ss = torch.empty((bsz, k), dtype=torch.float64, device=dev)
             Is = torch.empty((bsz, k), dtype=torch.int64, device=dev)
+            stream = torch.cuda.current_stream().cuda_stream
             for _ in range(2):
                 ix.search_device(Qs.data_ptr(), bsz, k, Ss.data_ptr(), Is.data_ptr(), stream=stream)
             ix.set_timing(True)

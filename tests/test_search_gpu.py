@@ -323,3 +323,31 @@ def test_ragged_tail_rows(hc):
                 s, i = ix.search(qs, 7)
                 es, ei = O.cosine_topk(qs, E.astype(np.float64), 7)
                 _check(s, i, es, ei)
+
+
+def test_llama_vector_store_dropin(hc):
+    """MI355XVectorStore.query vs the restated llama-index get_top_k_embeddings path."""
+    from types import SimpleNamespace
+    from hcrag_amd.llama_compat import MI355XVectorStore, TextNodeLite, VectorStoreQuery
+    rng = np.random.default_rng(31)
+    D, N = 384, 700
+    E = rng.standard_normal((N, D))
+    nodes = [TextNodeLite(id_=f"n{r}", text=f"t{r}", metadata={"type": "a" if r % 4 else "b"},
+                          embedding=E[r].tolist()) for r in range(N)]
+    vs = MI355XVectorStore(D, dtype="f32")
+    assert vs.add(nodes) == [f"n{r}" for r in range(N)]
+    q = E[5] + 0.1 * rng.standard_normal(D)
+    res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=10))
+    sims, ids = O.llama_get_top_k_embeddings(q.astype(np.float32), E.astype(np.float32), 10,
+                                             [f"n{r}" for r in range(N)])
+    assert res.ids == ids
+    np.testing.assert_allclose(res.similarities, sims, atol=1e-6)
+    flt = SimpleNamespace(filters=[SimpleNamespace(key="type", value="b", operator="==")])
+    res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=5, filters=flt))
+    keep = [r for r in range(N) if r % 4 == 0]
+    sims, ids = O.llama_get_top_k_embeddings(q.astype(np.float32), E[keep].astype(np.float32), 5,
+                                             [f"n{r}" for r in keep])
+    assert res.ids == ids
+    vs.delete("n0")
+    res = vs.query(VectorStoreQuery(query_embedding=E[0].tolist(), similarity_top_k=3))
+    assert "n0" not in res.ids
