@@ -53,6 +53,7 @@ static int set_err(int code, const char* fmt, ...) {
   } while (0)
 
 extern "C" const char* hcr_last_error(void) { return g_err.c_str(); }
+int hcr_set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
 extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.1.0 (gfx950)"; }
 extern "C" int hcr_device_count(void) {
   int n = 0;

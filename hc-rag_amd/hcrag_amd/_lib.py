@@ -64,6 +64,13 @@ _SIGS = {
     "hcr_index_set_timing": (c_int, [c_void_p, c_int]),
     "hcr_merge_topk_device": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
                                       c_void_p, c_void_p]),
+    "hcr_wordpiece_create": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p)]),
+    "hcr_wordpiece_create_from_buffer": (c_int, [c_char_p, c_int64, c_int, c_int,
+                                                 POINTER(c_void_p)]),
+    "hcr_wordpiece_destroy": (c_int, [c_void_p]),
+    "hcr_wordpiece_vocab_size": (c_int32, [c_void_p]),
+    "hcr_tokenize": (c_int, [c_void_p, POINTER(c_char_p), POINTER(c_int64), c_int64, c_int,
+                             POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
 }
 
 _lib = None

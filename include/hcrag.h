@@ -137,6 +137,25 @@ int hcr_index_set_timing(hcr_index* index, int enable);
 int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, int64_t nq,
                           int k, double* d_out_scores, int64_t* d_out_ids, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * WordPiece tokenizer (host).  Replaces HF tokenizers 0.21.1 (Rust) BertNormalizer +
+ * BertPreTokenizer + WordPiece reached through SentenceTransformer.encode
+ * (experiments/embedding_generator.py:124) / HuggingFaceEmbedding (graph_builder.py:147).
+ * ------------------------------------------------------------------------------------- */
+typedef struct hcr_tok hcr_tok;
+/* vocab.txt (one token per line, id = line number).  strip_accents: 1/0, or -1 = follow
+ * `lowercase` (BERT uncased default). */
+int hcr_wordpiece_create(const char* vocab_path, int lowercase, int strip_accents, hcr_tok** out);
+int hcr_wordpiece_create_from_buffer(const char* vocab_data, int64_t len, int lowercase,
+                                     int strip_accents, hcr_tok** out);
+int hcr_wordpiece_destroy(hcr_tok* tok);
+int32_t hcr_wordpiece_vocab_size(const hcr_tok* tok);
+/* Tokenise n UTF-8 strings (byte lengths in text_lens, or NULL for NUL-terminated): ids /
+ * mask are n x max_len ([CLS] .. [SEP], truncated, [PAD] padded), lengths[i] = tokens
+ * including the two specials. */
+int hcr_tokenize(const hcr_tok* tok, const char* const* texts, const int64_t* text_lens,
+                 int64_t n, int max_len, int32_t* ids, int32_t* mask, int32_t* lengths);
+
 #ifdef __cplusplus
 }
 #endif
