@@ -1,0 +1,316 @@
+// encoder.hip — host side of the BERT sentence-embedding C ABI (include/hcrag.h).
+//
+// Replaces SentenceTransformer('all-MiniLM-L6-v2').encode(...) (experiments/
+// embedding_generator.py:21,124,197,337; experiments/main.py:807,869) and
+// HuggingFaceEmbedding(model_name=...) (graph_builder.py:146-149, query_interface.py:136-137):
+// BertModel forward (transformers modeling_bert: embeddings -> N x [self-attention ->
+// dense+residual+LayerNorm -> dense+GELU -> dense+residual+LayerNorm]) followed by the
+// sentence-transformers Pooling (mean over the attention mask, or CLS) and Normalize.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "encoder_kernels.h"
+#include "hcrag.h"
+#include "host_common.h"
+
+using namespace hcr;
+
+struct EncLayer {
+  DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, wi, bi, wo2, bo2, ln2g, ln2b;
+};
+
+struct hcr_encoder {
+  int device = 0;
+  hcr_bert_config cfg{};
+  int dtype = HCR_F16;           // MFMA operand dtype (activations + projection weights)
+  hipStream_t stream = nullptr;
+  std::map<std::string, std::vector<float>> host;   // weights until finalize
+  bool ready = false;
+  DevBuf wemb, pemb, temb, embg, embb;
+  std::vector<EncLayer> layers;
+  // workspace
+  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out;
+  size_t att_lds_limit = 64 * 1024;
+};
+
+static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int compute_dtype,
+                                  hcr_encoder** out) {
+  if (!out || !cfg) return hcr_set_error(HCR_EINVAL, "NULL argument");
+  *out = nullptr;
+  const hcr_bert_config& c = *cfg;
+  if (c.hidden <= 0 || c.hidden % 64 || c.hidden > 4096)
+    return hcr_set_errorf(HCR_EINVAL, "hidden must be a positive multiple of 64 (<= 4096), got %d", c.hidden);
+  if (c.heads <= 0 || c.hidden % c.heads) return hcr_set_error(HCR_EINVAL, "hidden % heads != 0");
+  if (c.intermediate <= 0 || c.intermediate % 64) return hcr_set_error(HCR_EINVAL, "intermediate must be a multiple of 64");
+  if (c.layers <= 0 || c.vocab_size <= 0 || c.max_position <= 0 || c.type_vocab <= 0)
+    return hcr_set_error(HCR_EINVAL, "bad config sizes");
+  if (c.pooling != 0 && c.pooling != 1) return hcr_set_error(HCR_EINVAL, "pooling must be 0 (mean) or 1 (cls)");
+  if (compute_dtype != HCR_F16 && compute_dtype != HCR_BF16)
+    return hcr_set_error(HCR_EINVAL, "compute dtype must be HCR_F16 or HCR_BF16");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+  if (device < 0 || device >= ndev)
+    return hcr_set_errorf(HCR_EINVAL, "device %d not available (%d HIP devices)", device, ndev);
+  HIPC(hipSetDevice(device));
+  hcr_encoder* e = new hcr_encoder();
+  e->device = device;
+  e->cfg = c;
+  e->dtype = compute_dtype;
+  hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+  if (he != hipSuccess) {
+    delete e;
+    return hcr_set_errorf(HCR_EHIP, "hipStreamCreate: %s", hipGetErrorString(he));
+  }
+  *out = e;
+  return HCR_OK;
+}
+
+extern "C" int hcr_encoder_destroy(hcr_encoder* e) {
+  if (!e) return HCR_OK;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  DevBuf* bufs[] = {&e->wemb, &e->pemb, &e->temb, &e->embg, &e->embb, &e->ids, &e->mask, &e->x,
+                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out};
+  for (DevBuf* b : bufs) b->release();
+  for (auto& L : e->layers) {
+    DevBuf* lb[] = {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.ln1g, &L.ln1b, &L.wi, &L.bi, &L.wo2, &L.bo2, &L.ln2g, &L.ln2b};
+    for (DevBuf* b : lb) b->release();
+  }
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return HCR_OK;
+}
+
+// HF BertModel state-dict name, any prefix before "embeddings." / "encoder." is ignored
+// (sentence-transformers checkpoints use "0.auto_model." or none; BertForX uses "bert.").
+extern "C" int hcr_encoder_set_weight(hcr_encoder* e, const char* name, const float* data,
+                                      int64_t numel) {
+  if (!e || !name || (!data && numel > 0) || numel < 0) return hcr_set_error(HCR_EINVAL, "bad argument");
+  std::string n(name);
+  size_t p = n.find("embeddings.");
+  size_t q = n.find("encoder.");
+  if (q != std::string::npos && (p == std::string::npos || q < p)) p = q;
+  if (p == std::string::npos) return HCR_OK;    // pooler / heads: not used by the path
+  n = n.substr(p);
+  e->host[n].assign(data, data + numel);
+  e->ready = false;
+  return HCR_OK;
+}
+
+template <typename TM>
+static int upload_padded(DevBuf& dst, const std::vector<float>& src, int64_t rows, int64_t cols,
+                         int64_t rows_pad, hipStream_t st) {
+  CHECK(dst.ensure((size_t)rows_pad * cols * sizeof(TM)));
+  DevBuf tmp;
+  CHECK(tmp.ensure((size_t)rows * cols * 4));
+  HIPC(hipMemcpyAsync(tmp.p, src.data(), (size_t)rows * cols * 4, hipMemcpyHostToDevice, st));
+  const int64_t tot = rows_pad * cols;
+  hipLaunchKernelGGL((to_mfma_dtype<TM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                     tmp.as<const float>(), rows, rows_pad, (int)cols, dst.as<TM>());
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(st));
+  tmp.release();
+  return HCR_OK;
+}
+
+static int upload_f32(DevBuf& dst, const float* src, size_t n, size_t n_pad, hipStream_t st) {
+  CHECK(dst.ensure(n_pad * 4));
+  HIPC(hipMemsetAsync(dst.p, 0, n_pad * 4, st));
+  HIPC(hipMemcpyAsync(dst.p, src, n * 4, hipMemcpyHostToDevice, st));
+  return HCR_OK;
+}
+
+template <typename TM>
+static int finalize_t(hcr_encoder* e) {
+  const auto& c = e->cfg;
+  const int H = c.hidden, F = c.intermediate;
+  auto need = [&](const std::string& n, size_t numel, const std::vector<float>** out) -> int {
+    auto it = e->host.find(n);
+    if (it == e->host.end()) return hcr_set_errorf(HCR_EINVAL, "missing weight %s", n.c_str());
+    if (it->second.size() != numel)
+      return hcr_set_errorf(HCR_EINVAL, "weight %s has %zu elements, expected %zu", n.c_str(),
+                            it->second.size(), numel);
+    *out = &it->second;
+    return HCR_OK;
+  };
+  const std::vector<float> *we, *pe, *te, *eg, *eb;
+  CHECK(need("embeddings.word_embeddings.weight", (size_t)c.vocab_size * H, &we));
+  CHECK(need("embeddings.position_embeddings.weight", (size_t)c.max_position * H, &pe));
+  CHECK(need("embeddings.token_type_embeddings.weight", (size_t)c.type_vocab * H, &te));
+  CHECK(need("embeddings.LayerNorm.weight", H, &eg));
+  CHECK(need("embeddings.LayerNorm.bias", H, &eb));
+  hipStream_t st = e->stream;
+  CHECK(upload_f32(e->wemb, we->data(), we->size(), we->size(), st));
+  CHECK(upload_f32(e->pemb, pe->data(), pe->size(), pe->size(), st));
+  CHECK(upload_f32(e->temb, te->data(), te->size(), te->size(), st));
+  CHECK(upload_f32(e->embg, eg->data(), H, H, st));
+  CHECK(upload_f32(e->embb, eb->data(), H, H, st));
+  e->layers.clear();
+  e->layers.resize(c.layers);
+  for (int l = 0; l < c.layers; ++l) {
+    const std::string pfx = "encoder.layer." + std::to_string(l) + ".";
+    const std::vector<float> *wq, *bq, *wk, *bk, *wv, *bv, *wo, *bo, *g1, *b1, *wi, *bi, *wo2, *bo2, *g2, *b2;
+    CHECK(need(pfx + "attention.self.query.weight", (size_t)H * H, &wq));
+    CHECK(need(pfx + "attention.self.query.bias", H, &bq));
+    CHECK(need(pfx + "attention.self.key.weight", (size_t)H * H, &wk));
+    CHECK(need(pfx + "attention.self.key.bias", H, &bk));
+    CHECK(need(pfx + "attention.self.value.weight", (size_t)H * H, &wv));
+    CHECK(need(pfx + "attention.self.value.bias", H, &bv));
+    CHECK(need(pfx + "attention.output.dense.weight", (size_t)H * H, &wo));
+    CHECK(need(pfx + "attention.output.dense.bias", H, &bo));
+    CHECK(need(pfx + "attention.output.LayerNorm.weight", H, &g1));
+    CHECK(need(pfx + "attention.output.LayerNorm.bias", H, &b1));
+    CHECK(need(pfx + "intermediate.dense.weight", (size_t)F * H, &wi));
+    CHECK(need(pfx + "intermediate.dense.bias", F, &bi));
+    CHECK(need(pfx + "output.dense.weight", (size_t)H * F, &wo2));
+    CHECK(need(pfx + "output.dense.bias", H, &bo2));
+    CHECK(need(pfx + "output.LayerNorm.weight", H, &g2));
+    CHECK(need(pfx + "output.LayerNorm.bias", H, &b2));
+    EncLayer& L = e->layers[l];
+    std::vector<float> wqkv((size_t)3 * H * H), bqkv((size_t)3 * H);
+    std::memcpy(wqkv.data(), wq->data(), (size_t)H * H * 4);
+    std::memcpy(wqkv.data() + (size_t)H * H, wk->data(), (size_t)H * H * 4);
+    std::memcpy(wqkv.data() + (size_t)2 * H * H, wv->data(), (size_t)H * H * 4);
+    std::memcpy(bqkv.data(), bq->data(), H * 4);
+    std::memcpy(bqkv.data() + H, bk->data(), H * 4);
+    std::memcpy(bqkv.data() + 2 * H, bv->data(), H * 4);
+    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 128), st));
+    CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 128), st));
+    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 128), st));
+    CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 128), st));
+    CHECK(upload_f32(L.ln1g, g1->data(), H, H, st));
+    CHECK(upload_f32(L.ln1b, b1->data(), H, H, st));
+    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 128), st));
+    CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 128), st));
+    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 128), st));
+    CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 128), st));
+    CHECK(upload_f32(L.ln2g, g2->data(), H, H, st));
+    CHECK(upload_f32(L.ln2b, b2->data(), H, H, st));
+  }
+  HIPC(hipStreamSynchronize(st));
+  return HCR_OK;
+}
+
+extern "C" int hcr_encoder_finalize(hcr_encoder* e) {
+  if (!e) return hcr_set_error(HCR_EINVAL, "encoder is NULL");
+  HIPC(hipSetDevice(e->device));
+  int rc = e->dtype == HCR_F16 ? finalize_t<_Float16>(e) : finalize_t<__bf16>(e);
+  if (rc != HCR_OK) return rc;
+  e->host.clear();
+  e->ready = true;
+  return HCR_OK;
+}
+
+template <typename TM, int EPI>
+static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const float* bias,
+                       const float* resid, TM* out_h, float* out_f, int ldo, hipStream_t st) {
+  const int nft = (int)(rup(N, BR) / BR), ntt = (int)(rup(T, BQ) / BQ);
+  hipLaunchKernelGGL((gemm_nt_kernel<TM, EPI>), dim3((unsigned)(nft * ntt)), dim3(256), 0, st, W, X,
+                     K, N, T, nft, bias, resid, out_h, out_f, ldo);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+template <typename TM>
+static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask, int64_t n, int S,
+                    float* d_out, hipStream_t st) {
+  const auto& c = e->cfg;
+  const int H = c.hidden, F = c.intermediate, NH = c.heads, dh = H / NH;
+  const int64_t T = n * (int64_t)S, Tp = rup(T, 128);
+  if (T > (int64_t)1 << 30) return hcr_set_error(HCR_EINVAL, "batch too large");
+  CHECK(e->x.ensure((size_t)Tp * H * 4));
+  CHECK(e->y.ensure((size_t)Tp * H * 4));
+  CHECK(e->xh.ensure((size_t)Tp * H * sizeof(TM)));
+  CHECK(e->ctx.ensure((size_t)Tp * H * sizeof(TM)));
+  CHECK(e->qkv.ensure((size_t)Tp * 3 * H * sizeof(TM)));
+  CHECK(e->inter.ensure((size_t)Tp * F * sizeof(TM)));
+  const unsigned gT = (unsigned)((T + 3) / 4);
+  hipLaunchKernelGGL((embed_ln_kernel<TM>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+                     e->wemb.as<const float>(), e->pemb.as<const float>(),
+                     e->temb.as<const float>(), e->embg.as<const float>(),
+                     e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+  HIPC(hipGetLastError());
+  const size_t att_lds = (size_t)(5 * S + 4 * dh) * 4 + (size_t)2 * S * dh * sizeof(TM);
+  if (att_lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
+  if (att_lds > e->att_lds_limit) {
+    HIPC(hipFuncSetAttribute((const void*)attention_kernel<TM>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    e->att_lds_limit = 160 * 1024;
+  }
+  for (int l = 0; l < c.layers; ++l) {
+    const EncLayer& L = e->layers[l];
+    CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
+                                     L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
+                                     3 * H, st)));
+    hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * NH)), dim3(256), att_lds, st,
+                       e->qkv.as<const TM>(), d_mask, S, H, NH, e->ctx.as<TM>());
+    HIPC(hipGetLastError());
+    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H, (int)T,
+                                           L.bo.as<const float>(), e->x.as<const float>(), nullptr,
+                                           e->y.as<float>(), H, st)));
+    hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+                       (int)T, H, L.ln1g.as<const float>(), L.ln1b.as<const float>(),
+                       c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    HIPC(hipGetLastError());
+    CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
+                                          L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
+                                          nullptr, F, st)));
+    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F, H,
+                                           (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
+                                           nullptr, e->y.as<float>(), H, st)));
+    hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+                       (int)T, H, L.ln2g.as<const float>(), L.ln2b.as<const float>(),
+                       c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    HIPC(hipGetLastError());
+  }
+  hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st,
+                     e->x.as<const float>(), d_mask, S, H, c.pooling, c.normalize, d_out);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
+                                 int64_t n, int S, float* d_out, void* stream) {
+  if (!e) return hcr_set_error(HCR_EINVAL, "encoder is NULL");
+  if (!e->ready) return hcr_set_error(HCR_EINVAL, "encoder weights not finalized");
+  if (n < 0 || S <= 0) return hcr_set_error(HCR_EINVAL, "need n >= 0 and S > 0");
+  if (S > e->cfg.max_position) return hcr_set_errorf(HCR_EINVAL, "S=%d exceeds max_position %d", S, e->cfg.max_position);
+  if (n == 0) return HCR_OK;
+  if (!d_ids || !d_mask || !d_out) return hcr_set_error(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(e->device));
+  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  return e->dtype == HCR_F16 ? encode_t<_Float16>(e, d_ids, d_mask, n, S, d_out, st)
+                             : encode_t<__bf16>(e, d_ids, d_mask, n, S, d_out, st);
+}
+
+extern "C" int hcr_encode(hcr_encoder* e, const int32_t* ids, const int32_t* mask, int64_t n, int S,
+                          float* out) {
+  if (!e) return hcr_set_error(HCR_EINVAL, "encoder is NULL");
+  if (n == 0) return HCR_OK;
+  if (!ids || !mask || !out) return hcr_set_error(HCR_EINVAL, "NULL buffer");
+  if (n < 0 || S <= 0) return hcr_set_error(HCR_EINVAL, "need n >= 0 and S > 0");
+  HIPC(hipSetDevice(e->device));
+  const size_t T = (size_t)n * S;
+  CHECK(e->ids.ensure(T * 4));
+  CHECK(e->mask.ensure(T * 4));
+  CHECK(e->out.ensure((size_t)n * e->cfg.hidden * 4));
+  HIPC(hipMemcpyAsync(e->ids.p, ids, T * 4, hipMemcpyHostToDevice, e->stream));
+  HIPC(hipMemcpyAsync(e->mask.p, mask, T * 4, hipMemcpyHostToDevice, e->stream));
+  // ids must index the vocabulary: check on the host (an out-of-range id would read past the
+  // embedding table)
+  for (size_t i = 0; i < T; ++i)
+    if (ids[i] < 0 || ids[i] >= e->cfg.vocab_size)
+      return hcr_set_errorf(HCR_EINVAL, "token id %d out of range [0, %d)", ids[i], e->cfg.vocab_size);
+  CHECK(hcr_encode_device(e, e->ids.as<const int32_t>(), e->mask.as<const int32_t>(), n, S,
+                          e->out.as<float>(), e->stream));
+  HIPC(hipMemcpyAsync(out, e->out.p, (size_t)n * e->cfg.hidden * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPC(hipStreamSynchronize(e->stream));
+  return HCR_OK;
+}

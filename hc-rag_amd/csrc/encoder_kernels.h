@@ -1,0 +1,287 @@
+// encoder_kernels.h — HIP kernels of the BERT sentence-embedding forward (SURVEY.md §8(a)
+// a8-a9: tokenise -> embedding lookup -> encoder -> mean-pool -> L2-normalise).
+//
+// Replaces the torch-CPU BertModel + Pooling(mean) + Normalize of sentence-transformers
+// 4.1.0 / transformers 4.52.4 reached through SentenceTransformer.encode
+// (experiments/embedding_generator.py:124,197,337; experiments/main.py:807) and
+// HuggingFaceEmbedding (graph_builder.py:146-149).
+//
+// Layout: tokens T = B*S (padded to 128); residual stream x [T][H] fp32; its MFMA-dtype copy
+// xh [T][H]; projection weights W [N][K] exactly as HF nn.Linear stores them (K contiguous),
+// rows padded to 128 with zeros.  GEMM: C[feature][token] = W · xhᵀ on MFMA 16x16x32, so each
+// lane ends with 4 consecutive features of one token (16-byte bias / residual loads, 8-byte
+// f16 stores).
+#pragma once
+#include "device_common.h"
+#include "tile_common.h"   // MfmaOp, TileLoader (same LDS image and fragment reads as K2)
+
+namespace hcr {
+
+// -------------------------------------------------------------------------------------
+// Embedding gather + LayerNorm (one wave per token).  HF BertEmbeddings: word + position +
+// token_type(0), LayerNorm(eps), dropout (identity at inference).
+// -------------------------------------------------------------------------------------
+// row LayerNorm helper: values come from a functor (re-evaluated per pass; rows are L1-hot)
+template <typename TM, typename F>
+__device__ __forceinline__ void ln_row(F val, int H, const float* __restrict__ g,
+                                       const float* __restrict__ b, float eps, int lane,
+                                       float* __restrict__ xo, TM* __restrict__ xho) {
+  float s = 0.f;
+  for (int d = lane; d < H; d += 64) s += val(d);
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  const float mean = s / H;
+  float q = 0.f;
+  for (int d = lane; d < H; d += 64) { const float dd = val(d) - mean; q += dd * dd; }
+  for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, 64);
+  const float rstd = rsqrtf(q / H + eps);
+  for (int d = lane; d < H; d += 64) {
+    const float y = (val(d) - mean) * rstd * g[d] + b[d];
+    xo[d] = y;
+    xho[d] = (TM)y;
+  }
+}
+
+template <typename TM>
+__global__ void __launch_bounds__(256)
+embed_ln_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
+                const float* __restrict__ wemb, const float* __restrict__ pemb,
+                const float* __restrict__ temb, const float* __restrict__ g,
+                const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T_real) return;
+  const float* w = wemb + (size_t)ids[t] * H;
+  const float* p = pemb + (size_t)(t % S) * H;
+  ln_row<TM>([&](int d) { return w[d] + p[d] + temb[d]; }, H, g, b, eps, lane,
+             x + (size_t)t * H, xh + (size_t)t * H);
+}
+
+// LayerNorm of y (fp32, already = residual + sublayer output) -> x fp32 and xh MFMA dtype.
+template <typename TM>
+__global__ void __launch_bounds__(256)
+layernorm_kernel(const float* __restrict__ y, int T_real, int H, const float* __restrict__ g,
+                 const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T_real) return;
+  const float* yr = y + (size_t)t * H;
+  ln_row<TM>([&](int d) { return yr[d]; }, H, g, b, eps, lane, x + (size_t)t * H,
+             xh + (size_t)t * H);
+}
+
+// -------------------------------------------------------------------------------------
+// GEMM  C[token][feature] = sum_k xh[token][k] * W[feature][k] + bias[feature]  (+ epilogue)
+//   tile 128 features x 128 tokens, 4 waves (2 x 2), register-staged double-buffered LDS
+//   (same image / fragment reads as the score kernel v1).  M (features) and T (tokens) are
+//   padded to 128 by the caller; K % 64 == 0.
+// -------------------------------------------------------------------------------------
+enum : int { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESID = 2 };
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+template <typename TM, int EPI>
+__global__ void __launch_bounds__(256, 2)
+gemm_nt_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_real, int T_real,
+               int n_tiles_feat, const float* __restrict__ bias, const float* __restrict__ resid,
+               TM* __restrict__ out_h, float* __restrict__ out_f, int ldo) {
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  // XCD-friendly order: consecutive blocks share the token tile (X re-read from L2)
+  const int ft = blockIdx.x % n_tiles_feat, tt = blockIdx.x / n_tiles_feat;
+  const int f0 = ft * BR, t0 = tt * BQ;
+  const TM* Wt = W + (size_t)f0 * K;
+  const TM* Xt = X + (size_t)t0 * K;
+  TileLoader<TM> la, lb;
+  const int lr = lane & 15;
+  const int c0 = (lane >> 4) ^ (lane & 7);
+  const int offA0 = (wr * 64 + lr) * 128 + (c0 << 4);
+  const int offA1 = (wr * 64 + lr) * 128 + ((c0 ^ 4) << 4);
+  const int offB0 = (wc * 64 + lr) * 128 + (c0 << 4);
+  const int offB1 = (wc * 64 + lr) * 128 + ((c0 ^ 4) << 4);
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ksteps = K / BK;
+  la.load(Wt, 0, BR, K, 0, tid);
+  lb.load(Xt, 0, BQ, K, 0, tid);
+  la.store(lds, tid);
+  lb.store(lds + BR * 128, tid);
+  __syncthreads();
+  for (int s = 0; s < ksteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < ksteps;
+    if (more) {
+      la.load(Wt, 0, BR, K, (s + 1) * BK, tid);
+      lb.load(Xt, 0, BQ, K, (s + 1) * BK, tid);
+    }
+    const char* sa = lds + cur * STAGE_BYTES;
+    const char* sb = sa + BR * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int oa = kk ? offA1 : offA0, ob = kk ? offB1 : offB0;
+      V a[4], bq[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const V*>(sa + oa + m * 16 * 128);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(sb + ob + n * 16 * 128);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(a[m], bq[n], acc[m][n]);
+    }
+    if (more) {
+      char* st = lds + (cur ^ 1) * STAGE_BYTES;
+      la.store(st, tid);
+      lb.store(st + BR * 128, tid);
+    }
+    __syncthreads();
+  }
+  // epilogue: lane holds features f0 + wr*64 + m*16 + (lane>>4)*4 + r of token t0 + wc*64 + n*16 + lr
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int f = f0 + wr * 64 + m * 16 + (lane >> 4) * 4;
+    if (f >= N_real) continue;          // N_real % 4 == 0 (checked on the host)
+    const float4 bb = *reinterpret_cast<const float4*>(bias + f);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int t = t0 + wc * 64 + n * 16 + lr;
+      if (t >= T_real) continue;
+      float v0 = acc[m][n][0] + bb.x, v1 = acc[m][n][1] + bb.y;
+      float v2 = acc[m][n][2] + bb.z, v3 = acc[m][n][3] + bb.w;
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+      }
+      if constexpr (EPI == EPI_BIAS_RESID) {
+        const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
+        float4 o;
+        o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
+      } else {
+        TM* o = out_h + (size_t)t * ldo + f;
+        o[0] = (TM)v0; o[1] = (TM)v1; o[2] = (TM)v2; o[3] = (TM)v3;
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// Self-attention for one (sequence, head): softmax(Q Kᵀ / sqrt(dh) + mask) V.
+//   qkv [T][3H] (MFMA dtype: q | k | v), key mask from attention_mask (0 -> -inf, HF uses the
+//   dtype minimum; both give exactly 0 weight after softmax when any key is valid).
+//   One workgroup per (b, head); K and V of the sequence staged in LDS as fp32 (S*dh*8 bytes,
+//   S <= 256 at dh = 64); one wave per query row group; fp32 softmax.
+// -------------------------------------------------------------------------------------
+template <typename TM>
+__global__ void __launch_bounds__(256)
+attention_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, int S, int H,
+                 int heads, TM* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float att_sm[];
+  const int dh = H / heads;
+  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  float* Mk = att_sm;                                   // [S] additive key mask
+  float* Pw = Mk + S;                                   // [4 waves][S] probabilities
+  float* Qs = Pw + 4 * S;                               // [4 waves][dh] current query rows
+  TM* Ks = reinterpret_cast<TM*>(Qs + 4 * dh);          // [S][dh]
+  TM* Vs = Ks + (size_t)S * dh;                         // [S][dh]
+  const size_t row0 = (size_t)bidx * S;
+  const int ld3 = 3 * H;
+  for (int i = threadIdx.x; i < S * dh; i += blockDim.x) {
+    const int j = i / dh, d = i - j * dh;
+    const TM* base = qkv + (row0 + j) * ld3 + h * dh + d;
+    Ks[i] = base[H];
+    Vs[i] = base[2 * H];
+  }
+  for (int j = threadIdx.x; j < S; j += blockDim.x) Mk[j] = mask[row0 + j] ? 0.f : -INFINITY;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float scale = rsqrtf((float)dh);
+  float* pw = Pw + wave * S;
+  float* qs = Qs + wave * dh;
+  for (int i = wave; i < S; i += 4) {
+    const TM* qrow = qkv + (row0 + i) * ld3 + h * dh;
+    for (int d = lane; d < dh; d += 64) qs[d] = (float)qrow[d];
+    __builtin_amdgcn_wave_barrier();
+    float mx = -INFINITY;
+    for (int j = lane; j < S; j += 64) {
+      float acc = 0.f;
+      const TM* kr = Ks + (size_t)j * dh;
+      for (int d = 0; d < dh; ++d) acc += qs[d] * (float)kr[d];
+      const float sc = acc * scale + Mk[j];
+      pw[j] = sc;
+      mx = fmaxf(mx, sc);
+    }
+    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    float sum = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      const float e = (mx == -INFINITY) ? 0.f : __expf(pw[j] - mx);
+      pw[j] = e;
+      sum += e;
+    }
+    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    __builtin_amdgcn_wave_barrier();
+    for (int d = lane; d < dh; d += 64) {
+      float o = 0.f;
+      for (int j = 0; j < S; ++j) o += pw[j] * (float)Vs[(size_t)j * dh + d];
+      ctx[(row0 + i) * H + h * dh + d] = (TM)(o * inv);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// -------------------------------------------------------------------------------------
+// Pooling + L2 normalise (one block per sequence).
+//   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
+//   mode 1 (CLS, bge): h_0
+//   normalise: x / max(||x||, 1e-12)  (torch.nn.functional.normalize)
+// -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+pool_normalize_kernel(const float* __restrict__ x, const int32_t* __restrict__ mask, int S,
+                      int H, int mode, int normalize, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int bidx = blockIdx.x;
+  const size_t row0 = (size_t)bidx * S;
+  float cnt = 0.f;
+  if (mode == 0)
+    for (int t = 0; t < S; ++t) cnt += (float)mask[row0 + t];
+  const float denom = fmaxf(cnt, 1e-9f);
+  float local = 0.f;
+  for (int d = threadIdx.x; d < H; d += blockDim.x) {
+    float v;
+    if (mode == 0) {
+      v = 0.f;
+      for (int t = 0; t < S; ++t) v += x[(row0 + t) * H + d] * (float)mask[row0 + t];
+      v /= denom;
+    } else {
+      v = x[row0 * H + d];
+    }
+    out[(size_t)bidx * H + d] = v;
+    local += v * v;
+  }
+  red[threadIdx.x] = local;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (!normalize) return;
+  const float nrm = fmaxf(sqrtf(red[0]), 1e-12f);
+  for (int d = threadIdx.x; d < H; d += blockDim.x) out[(size_t)bidx * H + d] /= nrm;
+}
+
+// fp32 -> MFMA dtype conversion with zero padding of rows [rows, rows_pad)
+template <typename TM>
+__global__ void to_mfma_dtype(const float* __restrict__ src, int64_t rows, int64_t rows_pad,
+                              int cols, TM* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_pad * cols) return;
+  const int64_t r = i / cols;
+  dst[i] = r < rows ? (TM)src[i] : (TM)0.f;
+}
+
+}  // namespace hcr

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "hcrag.h"
+#include "host_common.h"
 #include "topk_kernels.h"
 
 using namespace hcr;
@@ -27,7 +28,7 @@ using namespace hcr;
 // ---------------------------------------------------------------------------------------
 static thread_local std::string g_err;
 
-static int set_err(int code, const char* fmt, ...) {
+int hcr_set_errorf(int code, const char* fmt, ...) {
   char buf[1024];
   va_list ap;
   va_start(ap, fmt);
@@ -36,21 +37,7 @@ static int set_err(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-#define HIPC(expr)                                                                       \
-  do {                                                                                   \
-    hipError_t e_ = (expr);                                                              \
-    if (e_ != hipSuccess) {                                                              \
-      return set_err(e_ == hipErrorOutOfMemory ? HCR_ENOMEM : HCR_EHIP, "%s: %s (%s:%d)", \
-                     #expr, hipGetErrorString(e_), __FILE__, __LINE__);                  \
-    }                                                                                    \
-  } while (0)
-
-#define CHECK(expr)              \
-  do {                           \
-    int rc_ = (expr);            \
-    if (rc_ != HCR_OK) return rc_; \
-  } while (0)
+#define set_err hcr_set_errorf
 
 extern "C" const char* hcr_last_error(void) { return g_err.c_str(); }
 int hcr_set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
@@ -64,25 +51,6 @@ extern "C" int hcr_device_count(void) {
 // ---------------------------------------------------------------------------------------
 // index object
 // ---------------------------------------------------------------------------------------
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  int ensure(size_t want) {
-    if (want <= bytes) return HCR_OK;
-    if (p) { HIPC(hipFree(p)); p = nullptr; bytes = 0; }
-    want = std::max<size_t>(want, 256);
-    HIPC(hipMalloc(&p, want));
-    bytes = want;
-    return HCR_OK;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
-};
-
 struct hcr_index {
   int device = 0;
   int dim = 0;

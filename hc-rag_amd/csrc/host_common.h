@@ -1,0 +1,45 @@
+// host_common.h — host-side helpers of libhcrag_hip.so: thread-local error, HIP checks,
+// owning device buffer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <string>
+
+#include "hcrag.h"
+
+int hcr_set_error(int code, const char* msg);    // defined in hcrag_index.hip
+int hcr_set_errorf(int code, const char* fmt, ...);
+
+#define HIPC(expr)                                                                          \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      return hcr_set_errorf(e_ == hipErrorOutOfMemory ? HCR_ENOMEM : HCR_EHIP, "%s: %s (%s:%d)", \
+                            #expr, hipGetErrorString(e_), __FILE__, __LINE__);              \
+    }                                                                                       \
+  } while (0)
+
+#define CHECK(expr)                \
+  do {                             \
+    int rc_ = (expr);              \
+    if (rc_ != HCR_OK) return rc_; \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t want) {
+    if (want <= bytes) return HCR_OK;
+    if (p) { HIPC(hipFree(p)); p = nullptr; bytes = 0; }
+    want = std::max<size_t>(want, 256);
+    HIPC(hipMalloc(&p, want));
+    bytes = want;
+    return HCR_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};

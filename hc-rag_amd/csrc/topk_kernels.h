@@ -13,29 +13,9 @@
 //   K5 merge_shards_kernel   g row-shards' exact top-k lists -> global top-k (multi-GPU).
 #pragma once
 #include "device_common.h"
+#include "tile_common.h"
 
 namespace hcr {
-
-constexpr int BR = 128;       // corpus rows per tile
-constexpr int BQ = 128;       // queries per block
-constexpr int BK = 64;        // K (embedding dim) per stage
-constexpr int NT = 256;       // threads per workgroup (4 waves, 2x2 over rows x queries)
-constexpr int STAGE_BYTES = (BR + BQ) * BK * 2;   // 32 KiB: A (rows) 16 KiB + B (queries) 16 KiB
-constexpr int LDS_STAGES = 2 * STAGE_BYTES;        // double buffered
-
-template <typename T> struct MfmaOp;
-template <> struct MfmaOp<_Float16> {
-  using V = half8;
-  static __device__ __forceinline__ floatx4 run(V a, V b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct MfmaOp<__bf16> {
-  using V = bf16x8;
-  static __device__ __forceinline__ floatx4 run(V a, V b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-};
 
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
 
@@ -133,74 +113,13 @@ prep_queries_kernel(const float* __restrict__ q32, int nq, int dim, int ld, TM* 
   }
 }
 
-// -------------------------------------------------------------------------------------
-// K2 helpers: global -> register -> LDS staging of one 128 x 64 tile (16 KiB, MFMA dtype).
-// LDS image: [row][8 chunks of 16 B], chunk slot = chunk ^ (row & 7)  (conflict-free for
-// the 16x16x32 fragment reads).
-// -------------------------------------------------------------------------------------
-template <typename TS> struct TileLoader;   // corpus rows in storage dtype TS
-
-// 16-bit storage: 4 x 16 B per thread.
-template <typename TS> struct TileLoader {
-  uint4 r[4];
-  __device__ __forceinline__ void load(const TS* __restrict__ base, int64_t row0, int64_t nrows,
-                                       int ld, int k0, int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      const int row = c >> 3, ch = c & 7;
-      int64_t gr = row0 + row;
-      gr = gr < nrows ? gr : nrows - 1;
-      r[i] = *reinterpret_cast<const uint4*>(base + gr * ld + k0 + ch * 8);
-    }
-  }
-  __device__ __forceinline__ void store(char* lds_tile, int tid) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      const int row = c >> 3, ch = c & 7;
-      *reinterpret_cast<uint4*>(lds_tile + row * 128 + ((ch ^ (row & 7)) << 4)) = r[i];
-    }
-  }
-};
-// f32 storage: 8 x 16 B per thread, converted to bf16 on the way into LDS.
-template <> struct TileLoader<float> {
-  float4 r[8];
-  __device__ __forceinline__ void load(const float* __restrict__ base, int64_t row0,
-                                       int64_t nrows, int ld, int k0, int tid) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      const int row = c >> 3, ch = c & 7;
-      int64_t gr = row0 + row;
-      gr = gr < nrows ? gr : nrows - 1;
-      const float4* p = reinterpret_cast<const float4*>(base + gr * ld + k0 + ch * 8);
-      r[2 * i] = p[0];
-      r[2 * i + 1] = p[1];
-    }
-  }
-  __device__ __forceinline__ void store(char* lds_tile, int tid) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = tid + NT * i;
-      const int row = c >> 3, ch = c & 7;
-      bf16x8 v;
-      v[0] = (__bf16)r[2 * i].x; v[1] = (__bf16)r[2 * i].y;
-      v[2] = (__bf16)r[2 * i].z; v[3] = (__bf16)r[2 * i].w;
-      v[4] = (__bf16)r[2 * i + 1].x; v[5] = (__bf16)r[2 * i + 1].y;
-      v[6] = (__bf16)r[2 * i + 1].z; v[7] = (__bf16)r[2 * i + 1].w;
-      *reinterpret_cast<bf16x8*>(lds_tile + row * 128 + ((ch ^ (row & 7)) << 4)) = v;
-    }
-  }
-};
-
 // Wave-cooperative compaction of one query's candidate buffer to its best `kp` keys.
 // Writes the sorted survivors back to `qbuf` (or to `out` when non-null, zero padded to kp),
 // updates the LDS count / local threshold and raises the global threshold.
 template <int CAP>
-__device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ qbuf, int* cnt_q,
-                                              uint64_t* tau_key_q, uint32_t* tau_g_q, int kp,
-                                              int lane, uint64_t* __restrict__ out) {
+__device__ __forceinline__ void compact_query_inl(uint64_t* __restrict__ qbuf, int* cnt_q,
+                                                  uint64_t* tau_key_q, uint32_t* tau_g_q, int kp,
+                                                  int lane, uint64_t* __restrict__ out) {
   constexpr int E = CAP / 64;
   const int c = *cnt_q;
   uint64_t v[E];
@@ -237,6 +156,14 @@ __device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ q
     *tau_key_q = kth;
     if (kth) atomicMax(tau_g_q, (uint32_t)(kth >> 32));
   }
+}
+
+template <int CAP>
+__device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ qbuf, int* cnt_q,
+                                                      uint64_t* tau_key_q, uint32_t* tau_g_q,
+                                                      int kp, int lane,
+                                                      uint64_t* __restrict__ out) {
+  compact_query_inl<CAP>(qbuf, cnt_q, tau_key_q, tau_g_q, kp, lane, out);
 }
 
 // -------------------------------------------------------------------------------------
@@ -505,7 +432,7 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int kp) {
+                     uint64_t* __restrict__ partials, int kp, float* __restrict__ dbg = nullptr) {
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   __shared__ __attribute__((aligned(16))) char lds[L2_TOTAL];
@@ -612,7 +539,7 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
         for (int ql = wave; ql < Q2; ql += NT2 / 64) {
           if (cnt[ql] > CAP - R2)
-            compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+            compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
                                tau_g + qbase + ql, kp, lane, nullptr);
         }
         __syncthreads();
@@ -662,6 +589,21 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       bool hit[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) hit[n] = mx[n] >= thr[n];
+#ifndef HCR_DBG_FINAL_RECORD
+      if (dbg) {                          // debug harness only: coarse scores [q][row]
+        for (int m = 0; m < MT2; ++m) {
+          float iv[4];
+          inv4(m, iv);
+          for (int n = 0; n < 4; ++n)
+            for (int r = 0; r < 4; ++r) {
+              const int64_t row = row0 + wm * (R2 / 2) + m * 16 + lq * 4 + r;
+              if (row < n_rows)
+                dbg[(size_t)(qbase + wn * 64 + n * 16 + lr) * n_rows + row] = acc[m][n][r] * iv[r];
+            }
+        }
+      }
+#endif
+#ifndef HCR_DBG_NO_APPEND
       if (__any(hit[0] | hit[1] | hit[2] | hit[3])) {
 #pragma unroll
         for (int m = 0; m < MT2; ++m) {
@@ -688,6 +630,7 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
           }
         }
       }
+#endif
 #pragma unroll
       for (int m = 0; m < MT2; ++m)
 #pragma unroll
@@ -698,6 +641,7 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
 
     // 3) MFMAs of step s
     const bool last_k = (ks == ksteps - 1);
+#ifndef HCR_DBG_NO_TG
     if (last_k) {
       int lt;
       asm volatile("v_mov_b32 %0, %1" : "=v"(lt) : "v"(lane));
@@ -706,6 +650,7 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         tg[n] = __hip_atomic_load(tau_g + qbase + wn * 64 + n * 16 + (lt & 15), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
     }
+#endif
     {
       const char* st = lds + (s & 1) * STAGE2;
 #pragma unroll
@@ -730,10 +675,26 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   }
 
   // final: every query's best kp keys -> partials[q][p][0..kp)
+#ifdef HCR_DBG_FINAL_RECORD
+  {
+    uint64_t* rec = reinterpret_cast<uint64_t*>(dbg);
+    for (int ql = wave; ql < Q2; ql += NT2 / 64) {
+      uint64_t* o = partials + ((size_t)(qbase + ql) * P + p) * kp;
+      const int c = cnt[ql];
+      if (lane == 0) {
+        rec[((size_t)(qbase + ql) * P + p) * 4 + 0] = (uint64_t)(uintptr_t)o;
+        rec[((size_t)(qbase + ql) * P + p) * 4 + 1] = (uint64_t)c;
+        rec[((size_t)(qbase + ql) * P + p) * 4 + 2] = (uint64_t)(uintptr_t)(wbuf + (size_t)ql * CAP);
+        rec[((size_t)(qbase + ql) * P + p) * 4 + 3] = (uint64_t)(uintptr_t)(tau_g + qbase + ql);
+      }
+    }
+  }
+#elif !defined(HCR_DBG_NO_FINAL)
   for (int ql = wave; ql < Q2; ql += NT2 / 64) {
-    compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
+    compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
                        lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
   }
+#endif
 }
 
 // -------------------------------------------------------------------------------------

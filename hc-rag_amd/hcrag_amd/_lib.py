@@ -35,7 +35,7 @@ class BertConfig(ctypes.Structure):
     """Mirror of ``hcr_bert_config`` (include/hcrag.h)."""
     _fields_ = [("vocab_size", c_int32), ("hidden", c_int32), ("layers", c_int32),
                 ("heads", c_int32), ("intermediate", c_int32), ("max_position", c_int32),
-                ("type_vocab", c_int32), ("pooling", c_int32), ("layer_norm_eps", c_float),
+                ("type_vocab", c_int32), ("layer_norm_eps", c_float), ("pooling", c_int32),
                 ("normalize", c_int32)]
 
 
@@ -71,6 +71,13 @@ _SIGS = {
     "hcr_wordpiece_vocab_size": (c_int32, [c_void_p]),
     "hcr_tokenize": (c_int, [c_void_p, POINTER(c_char_p), POINTER(c_int64), c_int64, c_int,
                              POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+    "hcr_encoder_create": (c_int, [c_int, POINTER(BertConfig), c_int, POINTER(c_void_p)]),
+    "hcr_encoder_destroy": (c_int, [c_void_p]),
+    "hcr_encoder_set_weight": (c_int, [c_void_p, c_char_p, c_void_p, c_int64]),
+    "hcr_encoder_finalize": (c_int, [c_void_p]),
+    "hcr_encode": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    "hcr_encode_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
+                                  c_void_p]),
 }
 
 _lib = None

@@ -156,6 +156,44 @@ int32_t hcr_wordpiece_vocab_size(const hcr_tok* tok);
 int hcr_tokenize(const hcr_tok* tok, const char* const* texts, const int64_t* text_lens,
                  int64_t n, int max_len, int32_t* ids, int32_t* mask, int32_t* lengths);
 
+/* ---------------------------------------------------------------------------------------
+ * BERT sentence encoder.  Replaces SentenceTransformer('all-MiniLM-L6-v2').encode
+ * (experiments/embedding_generator.py:21,124,197,337; experiments/main.py:807,869) and
+ * HuggingFaceEmbedding(model_name=...)._get_text_embeddings (graph_builder.py:146-149,
+ * query_interface.py:136-137): BertModel forward + Pooling(mean|cls) + Normalize.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t vocab_size;      /* 30522 for all-MiniLM-L6-v2 */
+  int32_t hidden;          /* 384; multiple of 64 */
+  int32_t layers;          /* 6 */
+  int32_t heads;           /* 12 */
+  int32_t intermediate;    /* 1536; multiple of 64 */
+  int32_t max_position;    /* 512 */
+  int32_t type_vocab;      /* 2 */
+  float layer_norm_eps;    /* 1e-12 */
+  int32_t pooling;         /* 0 = mean over attention mask (sentence-transformers), 1 = CLS */
+  int32_t normalize;       /* 1 = L2-normalise the pooled vector (Normalize module) */
+} hcr_bert_config;
+typedef struct hcr_encoder hcr_encoder;
+/* compute_dtype: HCR_F16 or HCR_BF16 (MFMA operands; accumulation, LayerNorm, softmax and
+ * the residual stream are fp32). */
+int hcr_encoder_create(int device, const hcr_bert_config* cfg, int compute_dtype,
+                       hcr_encoder** out);
+int hcr_encoder_destroy(hcr_encoder* enc);
+/* HF BertModel state-dict tensor (fp32, row-major as stored).  Any prefix before
+ * "embeddings." / "encoder." is ignored; pooler / head tensors are accepted and unused. */
+int hcr_encoder_set_weight(hcr_encoder* enc, const char* name, const float* data, int64_t numel);
+/* Upload all weights (checks every tensor of the config is present with the right size). */
+int hcr_encoder_finalize(hcr_encoder* enc);
+/* ids / mask: n x S int32 (token_type_ids are 0, as in SentenceTransformer.encode);
+ * out: n x hidden fp32.  Synchronous, host buffers. */
+int hcr_encode(hcr_encoder* enc, const int32_t* ids, const int32_t* mask, int64_t n, int S,
+               float* out);
+/* Same on device buffers, asynchronous on `stream` (NULL = the encoder's stream).  Ids must
+ * be in [0, vocab_size). */
+int hcr_encode_device(hcr_encoder* enc, const int32_t* d_ids, const int32_t* d_mask, int64_t n,
+                      int S, float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

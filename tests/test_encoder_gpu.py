@@ -1,0 +1,174 @@
+"""Encoder parity: the HIP BERT forward + mean-pool + L2 through the C
+ABI vs the engine the reference runs — transformers ``BertModel`` in fp32 on the CPU followed by
+sentence-transformers' Pooling(mean) + Normalize (experiments/embedding_generator.py:124).
+
+Weights are seeded random (no checkpoints offline) with LayerNorm parameters perturbed so the
+affine terms are exercised.  Tolerances (fp32 reference vs fp16/bf16 MFMA operands with fp32
+accumulation, LayerNorm, softmax and residual stream), stated per dtype below:
+  f16:  cosine(ours, ref) >= 0.9999 per sentence, max |diff| <= 4e-3 (unit vectors)
+  bf16: cosine(ours, ref) >= 0.999,  max |diff| <= 2e-2
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+transformers = pytest.importorskip("transformers")
+
+TOL = {"f16": (0.9999, 4e-3), "bf16": (0.999, 2e-2)}
+
+TINY = dict(vocab_size=211, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+            intermediate_size=256, max_position_embeddings=160, type_vocab_size=2)
+MINILM = dict(vocab_size=30522, hidden_size=384, num_hidden_layers=6, num_attention_heads=12,
+              intermediate_size=1536, max_position_embeddings=512, type_vocab_size=2)
+
+
+def _hf_model(cfg, seed):
+    torch.manual_seed(seed)
+    conf = transformers.BertConfig(**cfg, hidden_act="gelu", layer_norm_eps=1e-12,
+                                   hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m = transformers.BertModel(conf, add_pooling_layer=False).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if "LayerNorm" in n:
+                p.add_(0.1 * torch.randn_like(p))
+            elif n.endswith("bias"):
+                p.copy_(0.02 * torch.randn_like(p))
+    return conf, m
+
+
+def _ref_embed(m, ids, mask, pooling="mean", normalize=True):
+    with torch.no_grad():
+        h = m(input_ids=torch.from_numpy(ids.astype(np.int64)),
+              attention_mask=torch.from_numpy(mask.astype(np.int64))).last_hidden_state
+        if pooling == "mean":
+            mm = torch.from_numpy(mask).unsqueeze(-1).float()
+            v = (h * mm).sum(1) / mm.sum(1).clamp(min=1e-9)
+        else:
+            v = h[:, 0]
+        if normalize:
+            v = torch.nn.functional.normalize(v, p=2, dim=1)
+    return v.double().numpy()
+
+
+def _batch(rng, n, S, vocab, lens=None):
+    lens = rng.integers(1, S + 1, size=n) if lens is None else np.asarray(lens)
+    ids = np.zeros((n, S), np.int32)
+    mask = np.zeros((n, S), np.int32)
+    for i, L in enumerate(lens):
+        ids[i, :L] = rng.integers(5, vocab, size=L)
+        ids[i, 0], ids[i, L - 1] = 2, 3
+        mask[i, :L] = 1
+    return ids, mask
+
+
+def _check(ours, ref, dtype, normalize=True):
+    cmin, amax = TOL[dtype]
+    if normalize:
+        cos = np.sum(ours * ref, 1) / (np.linalg.norm(ours, axis=1) * np.linalg.norm(ref, axis=1))
+        assert cos.min() >= cmin, (cos.min(), dtype)
+        assert np.abs(ours - ref).max() <= amax, (np.abs(ours - ref).max(), dtype)
+    else:
+        rel = np.linalg.norm(ours - ref, axis=1) / np.linalg.norm(ref, axis=1)
+        assert rel.max() <= 1 - cmin + amax, rel.max()
+
+
+def _encoder(conf, m, dtype, pooling="mean", normalize=True):
+    from hcrag_amd import BertEncoder, config_from_hf
+    return BertEncoder(config_from_hf(conf.to_dict(), pooling, normalize), m.state_dict(),
+                       dtype=dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_tiny_ragged(dtype):
+    conf, m = _hf_model(TINY, 1)
+    rng = np.random.default_rng(0)
+    ids, mask = _batch(rng, 13, 37, TINY["vocab_size"], lens=[1, 2, 37, 36, 5, 17, 33, 3, 9, 10, 11, 12, 37])
+    enc = _encoder(conf, m, dtype)
+    _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask), dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_minilm_shape(dtype):
+    conf, m = _hf_model(MINILM, 2)
+    rng = np.random.default_rng(1)
+    ids, mask = _batch(rng, 24, 128, MINILM["vocab_size"])
+    enc = _encoder(conf, m, dtype)
+    _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask), dtype)
+
+
+@pytest.mark.gpu
+def test_cls_pooling_and_no_normalize():
+    conf, m = _hf_model(TINY, 3)
+    rng = np.random.default_rng(2)
+    ids, mask = _batch(rng, 9, 20, TINY["vocab_size"])
+    enc = _encoder(conf, m, "f16", pooling="cls", normalize=False)
+    _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask, "cls", False), "f16", False)
+
+
+@pytest.mark.gpu
+def test_padding_invariance_and_device_api():
+    conf, m = _hf_model(TINY, 5)
+    rng = np.random.default_rng(4)
+    ids, mask = _batch(rng, 6, 24, TINY["vocab_size"])
+    enc = _encoder(conf, m, "f16")
+    a = enc.encode_ids(ids, mask)
+    ids2 = np.pad(ids, ((0, 0), (0, 40)))
+    mask2 = np.pad(mask, ((0, 0), (0, 40)))
+    b = enc.encode_ids(ids2, mask2)
+    np.testing.assert_allclose(a, b, atol=2e-3)
+    dev = torch.device("cuda:0")
+    out = torch.empty((6, 128), dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    enc.encode_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), out,
+                      stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), a)
+
+
+@pytest.mark.gpu
+def test_sentence_embedder_surface():
+    """SentenceTransformer.encode semantics: length-sorted batches, input order kept."""
+    from hcrag_amd import SentenceEmbedder, WordPieceTokenizer
+    conf, m = _hf_model(TINY, 6)
+    words = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + [f"w{i}" for i in range(TINY["vocab_size"] - 5)]
+    tok = WordPieceTokenizer(vocab_tokens=words)
+    emb = SentenceEmbedder(tok, _encoder(conf, m, "f16"), max_seq_length=16, batch_size=3)
+    texts = ["w1 w2 w3", "w4", "w5 w6 w7 w8 w9 w10 w11 w12 w13 w14 w15 w16 w17 w18 w19",
+             "", "w7 w7", "W8 w9 zz", "w100"]
+    got = emb.encode(texts)
+    ids, mask, _ = tok.encode(texts, 16)
+    _check(got, _ref_embed(m, ids, mask), "f16")
+    assert emb.encode(texts[0]).shape == (128,)
+    e1 = np.asarray(emb.get_text_embedding(texts[2]))
+    np.testing.assert_allclose(e1, got[2], atol=2e-3)
+
+
+def test_encoder_rejects_bad_config():
+    """CPU: argument checks run before any device work."""
+    from hcrag_amd import BertEncoder, HcrError
+    bad = dict(vocab_size=10, hidden=100, layers=1, heads=2, intermediate=128, max_position=8,
+               type_vocab=2, layer_norm_eps=1e-12, pooling=0, normalize=1)
+    with pytest.raises((ValueError, HcrError)):
+        BertEncoder(bad, {}, dtype="f16")
+
+
+def test_config_from_hf():
+    from hcrag_amd import MINILM_L6_V2, config_from_hf
+    hf = dict(vocab_size=30522, hidden_size=384, num_hidden_layers=6, num_attention_heads=12,
+              intermediate_size=1536, max_position_embeddings=512, type_vocab_size=2,
+              layer_norm_eps=1e-12, hidden_act="gelu")
+    assert config_from_hf(hf) == MINILM_L6_V2
+    with pytest.raises(ValueError):
+        config_from_hf(dict(hf, hidden_act="relu"))
+
+
+@pytest.mark.gpu
+def test_long_sequence_512():
+    cfg = dict(TINY, max_position_embeddings=512, hidden_size=128, num_attention_heads=2)
+    conf, m = _hf_model(cfg, 4)
+    rng = np.random.default_rng(3)
+    ids, mask = _batch(rng, 3, 512, cfg["vocab_size"], lens=[512, 300, 1])
+    enc = _encoder(conf, m, "f16")
+    _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask), "f16")
