@@ -45,6 +45,10 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=32)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--encoder", default="bge-base", choices=["bge-base", "minilm", "none"],
+                   help="query-embedding leg: BERT shape (random init) encoded on each GPU")
+    p.add_argument("--enc-seq", type=int, default=32)
+    p.add_argument("--enc-steps", type=int, default=10)
     p.add_argument("--sweep", default="", help="comma list of batch sizes for an extra "
                    "1-GPU sweep printed to stderr (e.g. 1,8,32,64,256,1024)")
     return p.parse_args()
@@ -99,6 +103,87 @@ def cpu_baseline(E_rows_f16, Q, k, n_total):
             "sample": f"{nq} queries x {nr:,}-row slice of the same corpus (fp16 decoded to fp64), "
                       f"cosine_similarity fp64 + argsort[::-1][:{k}] in {t:.2f} s, "
                       f"extrapolated linearly to {n_total:,} rows"}
+
+
+ENC_SHAPES = {
+    # bge-base-en (768-d, the corpus dim of configs[2]; CLS pooling) and all-MiniLM-L6-v2
+    "bge-base": dict(vocab_size=30522, hidden=768, layers=12, heads=12, intermediate=3072,
+                     max_position=512, type_vocab=2, layer_norm_eps=1e-12, pooling=1, normalize=1),
+    "minilm": dict(vocab_size=30522, hidden=384, layers=6, heads=12, intermediate=1536,
+                   max_position=512, type_vocab=2, layer_norm_eps=1e-12, pooling=0, normalize=1),
+}
+
+
+def random_bert_state(cfg, seed=0):
+    """Random-init BERT weights (HF BertModel names; no checkpoints offline)."""
+    rng = np.random.default_rng(seed)
+    H, F = cfg["hidden"], cfg["intermediate"]
+
+    def w(*shape):
+        return (0.02 * rng.standard_normal(shape)).astype(np.float32)
+    sd = {"embeddings.word_embeddings.weight": w(cfg["vocab_size"], H),
+          "embeddings.position_embeddings.weight": w(cfg["max_position"], H),
+          "embeddings.token_type_embeddings.weight": w(cfg["type_vocab"], H),
+          "embeddings.LayerNorm.weight": np.ones(H, np.float32),
+          "embeddings.LayerNorm.bias": np.zeros(H, np.float32)}
+    for l in range(cfg["layers"]):
+        p = f"encoder.layer.{l}."
+        for nm in ("attention.self.query", "attention.self.key", "attention.self.value",
+                   "attention.output.dense"):
+            sd[p + nm + ".weight"], sd[p + nm + ".bias"] = w(H, H), w(H)
+        sd[p + "intermediate.dense.weight"], sd[p + "intermediate.dense.bias"] = w(F, H), w(F)
+        sd[p + "output.dense.weight"], sd[p + "output.dense.bias"] = w(H, F), w(H)
+        for nm in ("attention.output.LayerNorm", "output.LayerNorm"):
+            sd[p + nm + ".weight"] = np.ones(H, np.float32)
+            sd[p + nm + ".bias"] = np.zeros(H, np.float32)
+    return sd
+
+
+def encoder_leg(a, hc, dev, rank, world, dist):
+    """Query-embedding throughput: B query token sequences (S = --enc-seq, ragged lengths)
+    -> BERT forward -> pool -> L2 on each GPU; whole-job embeddings/s over max-over-ranks
+    time.  FLOPs per query = 2 * P_nonemb * S + 4 * L * S^2 * H."""
+    cfg = ENC_SHAPES[a.encoder]
+    enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=a.dtype, device=dev.index)
+    B, S = a.batch, a.enc_seq
+    g = torch.Generator(device="cpu").manual_seed(77 + rank)
+    ids = torch.randint(1000, cfg["vocab_size"], (B, S), generator=g, dtype=torch.int32)
+    lens = torch.randint(S // 2, S + 1, (B,), generator=g)
+    mask = (torch.arange(S)[None, :] < lens[:, None]).to(torch.int32)
+    ids = (ids * mask).to(dev)
+    mask = mask.to(dev)
+    out = torch.empty((B, cfg["hidden"]), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(2):
+        enc.encode_device(ids, mask, out, stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(a.enc_steps):
+        enc.encode_device(ids, mask, out, stream)
+    ev1.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    H, F, L = cfg["hidden"], cfg["intermediate"], cfg["layers"]
+    p_nonemb = L * (4 * H * H + 2 * H * F)
+    flops_q = 2.0 * p_nonemb * S + 4.0 * L * S * S * H
+    per_step = el / a.enc_steps
+    tf = B * flops_q / per_step / 1e12
+    norms = out.norm(dim=1)
+    enc.close()
+    return {"model": f"{a.encoder} shape, random init", "seq_len": S, "batch_per_gpu": B,
+            "query_embeddings_per_s": round(world * B / per_step, 1),
+            "ms_per_batch": round(per_step * 1e3, 3), "gpu_ms_per_batch": round(ev0.elapsed_time(ev1) / a.enc_steps, 3),
+            "flops_per_query": flops_q, "TFLOPs": round(tf, 2),
+            "mfma_frac": round(tf / MFMA_PEAK_TFLOPS, 4),
+            "unit_norm_ok": bool(((norms - 1).abs() < 1e-3).all().item())}
 
 
 def main():
@@ -200,6 +285,10 @@ def main():
         cpu = cpu_baseline(Eh, Q[: a.cpu_queries].cpu().numpy(), k, N)
         del Eh
 
+    enc_res = None
+    if a.encoder != "none":
+        enc_res = encoder_leg(a, hc, dev, rank, world, dist)
+
     if a.sweep and world == 1 and rank == 0:
         for bsz in [int(x) for x in a.sweep.split(",") if x]:
             Qs = torch.randn((bsz, D), device=dev)
@@ -240,6 +329,7 @@ def main():
                        "parallelism": f"rowshard{world}" + ("+rccl_allgather_alltoall" if world > 1 else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "encoder": enc_res,
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
                       "widened_queries": widened, "kprime": st["kprime"],
                       "partitions": st["partitions"], "workgroups": st["workgroups"],

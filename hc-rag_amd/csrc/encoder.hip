@@ -285,7 +285,7 @@ extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int
   if (n == 0) return HCR_OK;
   if (!d_ids || !d_mask || !d_out) return hcr_set_error(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(e->device));
-  hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+  hipStream_t st = (hipStream_t)stream;   // the caller's stream (NULL = legacy default)
   return e->dtype == HCR_F16 ? encode_t<_Float16>(e, d_ids, d_mask, n, S, d_out, st)
                              : encode_t<__bf16>(e, d_ids, d_mask, n, S, d_out, st);
 }

@@ -422,8 +422,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, 
 }
 __device__ __forceinline__ void* uniform_ptr(const void* p) {
   const uint64_t v = (uint64_t)p;
-  return (void*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-                 (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v));
+  // readfirstlane returns a signed int: go through uint32_t so an address whose low word has
+  // bit 31 set is not sign-extended into the high word
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  return (void*)(((uint64_t)hi << 32) | (uint64_t)lo);
 }
 
 template <typename TM, int CAP>
@@ -674,7 +677,9 @@ score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     ks = nks;
   }
 
-  // final: every query's best kp keys -> partials[q][p][0..kp)
+  // final: every query's best kp keys -> partials[q][p][0..kp).  Both row halves (wm) of
+  // the last epilogue append to the same queries: wait for all of them.
+  __syncthreads();
 #ifdef HCR_DBG_FINAL_RECORD
   {
     uint64_t* rec = reinterpret_cast<uint64_t*>(dbg);

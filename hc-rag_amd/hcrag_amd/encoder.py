@@ -104,13 +104,16 @@ class BertEncoder:
 
     def encode_device(self, ids, mask, out, stream: Optional[int] = None) -> None:
         """Device tensors (torch, int32 [n, S] / fp32 [n, hidden]); async on ``stream``
-        (a raw hipStream_t handle, default: the encoder's own stream)."""
+        (a raw hipStream_t handle, default: torch's current stream)."""
         n, S = ids.shape
         if tuple(mask.shape) != (n, S) or tuple(out.shape) != (n, self.hidden):
             raise ValueError("shape mismatch")
         for t, dt in ((ids, "int32"), (mask, "int32"), (out, "float32")):
             if str(t.dtype).split(".")[-1] != dt or not t.is_contiguous() or not t.is_cuda:
                 raise ValueError(f"expected contiguous {dt} device tensors")
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(out.device).cuda_stream
         check(lib().hcr_encode_device(self._h, ids.data_ptr(), mask.data_ptr(), n, S,
                                       out.data_ptr(), stream))
 
@@ -203,3 +206,45 @@ class SentenceEmbedder:
 
     def get_agg_embedding_from_queries(self, queries: Sequence[str]) -> List[float]:
         return np.mean(self.encode(list(queries)), axis=0).tolist()
+
+
+class MI355XEmbedding(SentenceEmbedder):
+    """``HuggingFaceEmbedding`` field/method surface (SURVEY.md §8(a) a9;
+    graph_builder.py:146-149, query_interface.py:136-137): ``model_name``,
+    ``embed_batch_size`` (llama-index default 10), embeddings always L2-normalised
+    (``normalize_embeddings=True``), optional query / text instruction prefixes (bge-*-en)."""
+
+    def __init__(self, model_name: str, embed_batch_size: int = 10, dtype: str = "f16",
+                 device: int = 0, max_length: Optional[int] = None,
+                 query_instruction: Optional[str] = None, text_instruction: Optional[str] = None,
+                 pooling: str = "mean"):
+        base = SentenceEmbedder.from_pretrained(model_name, dtype=dtype, device=device,
+                                                max_seq_length=max_length,
+                                                batch_size=embed_batch_size, pooling=pooling)
+        super().__init__(base.tokenizer, base.encoder, base.max_seq_length, embed_batch_size)
+        self.model_name = model_name
+        self.embed_batch_size = int(embed_batch_size)
+        self.query_instruction = query_instruction
+        self.text_instruction = text_instruction
+
+    def _fmt(self, text: str, instr: Optional[str]) -> str:
+        return f"{instr} {text}".strip() if instr else text
+
+    def _get_query_embedding(self, query: str) -> List[float]:
+        return self.encode([self._fmt(query, self.query_instruction)],
+                           normalize_embeddings=True)[0].tolist()
+
+    def _get_text_embedding(self, text: str) -> List[float]:
+        return self.encode([self._fmt(text, self.text_instruction)],
+                           normalize_embeddings=True)[0].tolist()
+
+    def _get_text_embeddings(self, texts: List[str]) -> List[List[float]]:
+        return self.encode([self._fmt(t, self.text_instruction) for t in texts],
+                           normalize_embeddings=True).tolist()
+
+    get_query_embedding = _get_query_embedding
+    get_text_embedding = _get_text_embedding
+
+    def get_text_embedding_batch(self, texts: Sequence[str], show_progress: bool = False,
+                                 **_) -> List[List[float]]:
+        return self._get_text_embeddings(list(texts))

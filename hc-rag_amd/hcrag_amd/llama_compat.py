@@ -208,5 +208,45 @@ class MI355XVectorRetriever:
         return list(zip(res.nodes, res.similarities))
 
 
-__all__ = ["MI355XVectorStore", "MI355XVectorRetriever", "VectorStoreQuery",
+class MI355XPropertyGraphStore:
+    """Vector half of a ``PropertyGraphStore`` (second form):
+    ``supports_vector_queries = True`` and ``vector_query(VectorStoreQuery) -> (nodes,
+    scores)``, the call ``VectorContextRetriever`` makes instead of a separate vector store
+    when the graph store holds the node embeddings (``SimplePropertyGraphStore`` at
+    graph_builder.py:161 keeps them on ``LabelledNode.embedding``).  Triplets / relations stay
+    with the caller's graph store; ``get(ids=...)`` returns the stored node objects."""
+
+    supports_structured_queries: bool = False
+    supports_vector_queries: bool = True
+
+    def __init__(self, dim: int, dtype: str = "f16", device: int = 0):
+        self._vs = MI355XVectorStore(dim, dtype=dtype, device=device)
+        self._by_id: Dict[str, Any] = {}
+
+    def upsert_nodes(self, nodes: Sequence[Any]) -> None:
+        fresh = []
+        for n in nodes:
+            nid = _node_id(n)
+            if nid in self._by_id:
+                self._vs.delete(nid)
+            self._by_id[nid] = n
+            if getattr(n, "embedding", None) is not None:
+                fresh.append(n)
+        if fresh:
+            self._vs.add(fresh)
+
+    def get(self, properties: Optional[dict] = None, ids: Optional[List[str]] = None) -> List[Any]:
+        out = [self._by_id[i] for i in (ids or list(self._by_id)) if i in self._by_id]
+        if properties:
+            out = [n for n in out if all((getattr(n, "properties", None) or
+                                          getattr(n, "metadata", {}) or {}).get(k) == v
+                                         for k, v in properties.items())]
+        return out
+
+    def vector_query(self, query, **kwargs):
+        res = self._vs.query(query)
+        return list(res.nodes), list(res.similarities)
+
+
+__all__ = ["MI355XVectorStore", "MI355XVectorRetriever", "MI355XPropertyGraphStore", "VectorStoreQuery",
            "VectorStoreQueryResult", "TextNodeLite", "HAVE_LLAMA"]

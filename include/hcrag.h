@@ -189,8 +189,8 @@ int hcr_encoder_finalize(hcr_encoder* enc);
  * out: n x hidden fp32.  Synchronous, host buffers. */
 int hcr_encode(hcr_encoder* enc, const int32_t* ids, const int32_t* mask, int64_t n, int S,
                float* out);
-/* Same on device buffers, asynchronous on `stream` (NULL = the encoder's stream).  Ids must
- * be in [0, vocab_size). */
+/* Same on device buffers, asynchronous on `stream` (a hipStream_t; NULL = the legacy default
+ * stream).  Ids must be in [0, vocab_size). */
 int hcr_encode_device(hcr_encoder* enc, const int32_t* d_ids, const int32_t* d_mask, int64_t n,
                       int S, float* d_out, void* stream);
 

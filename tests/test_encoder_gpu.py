@@ -172,3 +172,26 @@ def test_long_sequence_512():
     ids, mask = _batch(rng, 3, 512, cfg["vocab_size"], lens=[512, 300, 1])
     enc = _encoder(conf, m, "f16")
     _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask), "f16")
+
+
+@pytest.mark.gpu
+def test_from_pretrained_snapshot_dir(tmp_path):
+    """HuggingFaceEmbedding surface from a local snapshot (config.json + model.safetensors +
+    vocab.txt + 1_Pooling/config.json), as graph_builder.py:146-149 would load it."""
+    import json
+    from hcrag_amd import MI355XEmbedding, WordPieceTokenizer
+    conf, m = _hf_model(TINY, 7)
+    m.save_pretrained(str(tmp_path), safe_serialization=True)
+    words = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"] + [f"t{i}" for i in range(TINY["vocab_size"] - 5)]
+    (tmp_path / "vocab.txt").write_text("\n".join(words) + "\n")
+    (tmp_path / "1_Pooling").mkdir()
+    (tmp_path / "1_Pooling" / "config.json").write_text(json.dumps({"pooling_mode_mean_tokens": True}))
+    (tmp_path / "sentence_bert_config.json").write_text(json.dumps({"max_seq_length": 24}))
+    emb = MI355XEmbedding(str(tmp_path), embed_batch_size=2)
+    texts = ["t1 t2 t3 t4", "t9", "t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3 t3"]
+    got = np.asarray(emb.get_text_embedding_batch(texts))
+    ids, mask, _ = WordPieceTokenizer(vocab_tokens=words).encode(texts, 24)
+    _check(got, _ref_embed(m, ids, mask), "f16")
+    q = np.asarray(emb.get_query_embedding("t9"))
+    np.testing.assert_allclose(q, got[1], atol=2e-3)
+    assert emb.max_seq_length == 24 and emb.model_name == str(tmp_path)

@@ -351,3 +351,23 @@ def test_llama_vector_store_dropin(hc):
     vs.delete("n0")
     res = vs.query(VectorStoreQuery(query_embedding=E[0].tolist(), similarity_top_k=3))
     assert "n0" not in res.ids
+
+
+@pytest.mark.gpu
+def test_property_graph_store_vector_query():
+    """PropertyGraphStore.vector_query form of the boundary."""
+    from hcrag_amd.llama_compat import MI355XPropertyGraphStore, TextNodeLite, VectorStoreQuery
+    rng = np.random.default_rng(11)
+    E = rng.standard_normal((300, 64)).astype(np.float32)
+    nodes = [TextNodeLite(id_=f"n{i}", embedding=E[i].tolist(), metadata={"type": "t%d" % (i % 3)})
+             for i in range(300)]
+    gs = MI355XPropertyGraphStore(64, dtype="f32")
+    gs.upsert_nodes(nodes)
+    assert gs.supports_vector_queries
+    q = rng.standard_normal(64).astype(np.float32)
+    got_nodes, got_scores = gs.vector_query(VectorStoreQuery(query_embedding=q.tolist(),
+                                                             similarity_top_k=7))
+    s, ids = O.cosine_topk(q[None].astype(np.float64), E.astype(np.float64), 7)
+    assert [n.node_id for n in got_nodes] == [f"n{i}" for i in ids[0]]
+    np.testing.assert_allclose(got_scores, s[0], atol=1e-6)
+    assert [n.node_id for n in gs.get(ids=["n3", "n5"])] == ["n3", "n5"]
