@@ -20,6 +20,7 @@
 #include "hcrag.h"
 #include "host_common.h"
 #include "topk_kernels.h"
+#include "score_v3.h"
 
 using namespace hcr;
 
@@ -394,6 +395,59 @@ static int dispatch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, 
   return HCR_OK;
 }
 
+// ---- K2 v3 (score_v3.h): tile configurations by batch size ----
+struct V3Cfg { int rt, qt, nst; };
+static V3Cfg v3_cfg(int nq) {
+  if (nq <= 16) return {256, 16, 8};
+  if (nq <= 64) return {256, 64, 7};
+  if (nq <= 128) return {256, 128, 6};
+  static const int nst_large = [] {      // HCRAG_V3_NST=3|4|5: ring depth of the large shape
+    const char* e = getenv("HCRAG_V3_NST");
+    const int v = e ? atoi(e) : 5;
+    return (v >= 3 && v <= 5) ? v : 5;
+  }();
+  return {224, 256, nst_large};
+}
+// the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
+// outlive NST-1 stages of look-ahead
+static bool v3_fits(const hcr_index* ix, V3Cfg c) {
+  return (V3_NIS - 1) * (ix->ld / V3_BK) > c.nst - 1;
+}
+
+struct V3Launch { int nqb, P, nvt, tstride, kp; };
+
+template <typename TM, int CAP, int RT, int QT, int WM, int WN, int NST>
+static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
+  hipLaunchKernelGGL((score_topk_v3_kernel<TM, CAP, RT, QT, WM, WN, NST>), dim3(a.nqb * a.P),
+                     dim3(V3_NT), 0, st, ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                     ix->inv32.as<const float>(),
+                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                     ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                     ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                     ix->w_part.as<uint64_t>(), a.kp);
+}
+
+template <typename TM, int CAP>
+static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
+  if (c.qt == 256 && c.nst == 3) launch_v3_t<TM, CAP, 224, 256, 2, 4, 3>(ix, a, st);
+  else if (c.qt == 256 && c.nst == 4) launch_v3_t<TM, CAP, 224, 256, 2, 4, 4>(ix, a, st);
+  else if (c.qt == 256) launch_v3_t<TM, CAP, 224, 256, 2, 4, 5>(ix, a, st);
+  else if (c.qt == 128) launch_v3_t<TM, CAP, 256, 128, 4, 2, 6>(ix, a, st);
+  else if (c.qt == 64) launch_v3_t<TM, CAP, 256, 64, 4, 2, 7>(ix, a, st);
+  else launch_v3_t<TM, CAP, 256, 16, 8, 1, 8>(ix, a, st);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+template <typename TM>
+static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
+  switch (cap) {
+    case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
+    case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
+    default: return set_err(HCR_EINVAL, "internal: unsupported candidate capacity %d", cap);
+  }
+}
+
 template <typename TS>
 static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d_q, int nq, int kp, int k, int mode,
                            double thr, double* out_s, int64_t* out_i, hipStream_t st) {
@@ -404,22 +458,69 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>());
 }
 
+static constexpr int kSampleStride = 16;          // pre-pass samples 1 row tile in 16
+static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgroup has >= 32 tiles
+
+// tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
+__global__ void seed_tau_kernel(const uint64_t* __restrict__ merged, int nq, int kp,
+                                uint32_t* __restrict__ tau_g) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nq) return;
+  const uint64_t kth = merged[(size_t)q * kp + kp - 1];
+  tau_g[q] = kth ? (uint32_t)(kth >> 32) : 0u;
+}
+
+// Tree merge of the per-partition lists in ix->w_part ([q][P][kp]) into one sorted top-kp list
+// per query ([q][kp]); groups of G lists per block, ping-ponging through ix->w_merged.
+static int merge_tree(hcr_index* ix, int nq, int nqpad, int P, int P2, int G, int kp,
+                      hipStream_t st, const uint64_t** out) {
+  const uint64_t* src = ix->w_part.as<const uint64_t>();
+  uint64_t* bufs[2] = {ix->w_merged.as<uint64_t>(),
+                       ix->w_merged.as<uint64_t>() + (size_t)nqpad * std::max(P2, 1) * kp};
+  int which = 0, pin = P;
+  while (true) {
+    const int pout = (pin + G - 1) / G;
+    const int M = next_pow2(std::min(G, pin) * kp);
+    uint64_t* dst = bufs[which];
+    hipLaunchKernelGGL(merge_partials_kernel, dim3(nq, pout), dim3(256), (size_t)M * 8, st,
+                       src, pin, G, kp, M, dst);
+    HIPC(hipGetLastError());
+    src = dst;
+    which ^= 1;
+    if (pout == 1) break;
+    pin = pout;
+  }
+  *out = src;
+  return HCR_OK;
+}
+
 // One pipeline pass over nq (<= kQueryChunk) device queries at candidate depth kp.
 // Returns the number of uncertified queries in *n_unc (stream is synchronised).
 static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode, double thr,
                        double* d_out_s, int64_t* d_out_i, int kp, hipStream_t st, int* n_unc,
                        std::vector<int>* unc_list) {
   const uint64_t* merged_ptr = nullptr;
-  // kernel choice: v2 (256 x 256 tiles, LDS-DMA) for large batches of 16-bit rows,
-  // v1 (128 x 128 tiles) for small batches and f32 rows.
-  static const bool v2_disabled = getenv("HCRAG_DISABLE_V2") != nullptr;
-  const bool v2 = !v2_disabled && ix->dtype != HCR_F32 && nq >= kV2MinQueries;
-  const int tq = v2 ? Q2 : BQ, tr = v2 ? R2 : BR;
+  // kernel choice (HCRAG_SCORE_KERNEL=v1|v2|v3 overrides): v3 (deep LDS-DMA ring, tile shape
+  // by batch size) for 16-bit rows; v1 (register-staged 128 x 128, converts fp32 rows to
+  // bf16 on the way into LDS) for fp32 rows.
+  static const int forced = [] {
+    const char* e = getenv("HCRAG_SCORE_KERNEL");
+    if (getenv("HCRAG_DISABLE_V2")) return 1;
+    if (!e) return 0;
+    return e[0] == 'v' ? atoi(e + 1) : 0;
+  }();
+  int ver = ix->dtype == HCR_F32 ? 1 : (forced ? forced : 3);
+  if (ver == 2 && nq < kV2MinQueries) ver = 1;
+  if (ix->dtype == HCR_F32) ver = 1;
+  const V3Cfg c3 = v3_cfg(nq);
+  if (ver == 3 && !v3_fits(ix, c3)) ver = 1;
+  const bool v2 = ver == 2;
+  const int tq = ver == 3 ? c3.qt : v2 ? Q2 : BQ, tr = ver == 3 ? c3.rt : v2 ? R2 : BR;
   const int nqpad = (int)round_up(nq, tq);
   const int nqb = nqpad / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
   const int cap = next_pow2(kp + tr);
-  const int wg_target = v2 ? 256 : 512;
+  const int wg_target = ver == 1 ? 512 : 256;
   int P = std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
@@ -469,7 +570,31 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   HIPC(hipGetLastError());
 
   if (ix->timing) HIPC(hipEventRecord(ix->ev0, st));
-  if (v2) {
+  if (ver == 3) {
+    // Sampling pre-pass (every kSampleStride-th row tile): the k'-th best coarse key of the
+    // sample is <= the global k'-th best coarse key, so it seeds the per-query global bound
+    // tau_g exactly; the dense pass then appends only rows that can still be in the top-k'.
+    static const bool no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
+    static const int min_tiles = [] {    // HCRAG_PREPASS_MIN_TILES: tests force the pre-pass
+      const char* e = getenv("HCRAG_PREPASS_MIN_TILES");
+      return e ? std::max(1, atoi(e)) : kPrepassMinTilesPerWg;
+    }();
+    if (!no_prepass && ntiles >= (int64_t)P * min_tiles) {
+      V3Launch a{nqb, 0, (ntiles + kSampleStride - 1) / kSampleStride, kSampleStride, kp};
+      a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
+      a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
+      if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
+      else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
+      const uint64_t* sample_best = nullptr;
+      CHECK(merge_tree(ix, nq, nqpad, a.P, P2, G, kp, st, &sample_best));
+      hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
+                         sample_best, nq, kp, ix->w_taug.as<uint32_t>());
+      HIPC(hipGetLastError());
+    }
+    const V3Launch a{nqb, P, (int)ntiles, 1, kp};
+    if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
+    else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
+  } else if (v2) {
     if (ix->dtype == HCR_F16) CHECK((dispatch_score256<_Float16>(ix, nqb, P, ntiles, kp, cap, st)));
     else CHECK((dispatch_score256<__bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   } else if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
@@ -477,26 +602,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
-  // tree merge: groups of G partition lists -> one list, until one list per query remains
-  {
-    const uint64_t* src = ix->w_part.as<const uint64_t>();
-    uint64_t* bufs[2] = {ix->w_merged.as<uint64_t>(),
-                         ix->w_merged.as<uint64_t>() + (size_t)nqpad * std::max(P2, 1) * kp};
-    int which = 0, pin = P;
-    while (true) {
-      const int pout = (pin + G - 1) / G;
-      const int M = next_pow2(std::min(G, pin) * kp);
-      uint64_t* dst = bufs[which];
-      hipLaunchKernelGGL(merge_partials_kernel, dim3(nq, pout), dim3(256), (size_t)M * 8, st,
-                         src, pin, G, kp, M, dst);
-      HIPC(hipGetLastError());
-      src = dst;
-      which ^= 1;
-      if (pout == 1) break;
-      pin = pout;
-    }
-    merged_ptr = src;
-  }
+  CHECK(merge_tree(ix, nq, nqpad, P, P2, G, kp, st, &merged_ptr));
 
   if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);

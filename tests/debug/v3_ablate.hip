@@ -1,0 +1,65 @@
+// Timing-only ablation of score_topk_v3_kernel at the bench shape (10M x 768 f16 rows,
+// 1024 queries, k' = 64): build with -DHCR_V3_NO_DMA / -DHCR_V3_NO_MFMA / -DHCR_V3_NO_EPI
+// and compare kernel times (outputs are not checked here; tests/test_search_gpu.py does).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include "../../hc-rag_amd/csrc/score_v3.h"
+using namespace hcr;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 2; } } while (0)
+
+__global__ void fill_rows(_Float16* r, int64_t n, uint32_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+  x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+  r[i] = (_Float16)(((int)(x & 0xFFFF) - 32768) * (1.0f / 32768.f) * 0.036f);
+}
+__global__ void fill_f(float* p, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+template <int RT, int QT, int WM, int WN, int NST>
+static int run(const char* name, int64_t N, int nq, int reps) {
+  const int ld = 768, kp = 64, CAP = 512;
+  const int nqpad = (nq + QT - 1) / QT * QT, nqb = nqpad / QT;
+  const int ntiles = (int)((N + RT - 1) / RT);
+  int P = std::max(1, (256 + nqb - 1) / nqb);
+  P = std::min(P, ntiles);
+  const int nwg = nqb * P;
+  const int64_t arows = (N + 255) / 256 * 256 + 512;
+  _Float16 *rows, *q; float* inv; uint64_t *buf, *part; uint32_t* tau;
+  CK(hipMalloc(&rows, arows * ld * 2)); CK(hipMalloc(&q, (size_t)nqpad * ld * 2));
+  CK(hipMalloc(&inv, arows * 4)); CK(hipMalloc(&buf, (size_t)nwg * QT * CAP * 8));
+  CK(hipMalloc(&part, (size_t)nqpad * P * kp * 8)); CK(hipMalloc(&tau, nqpad * 4));
+  hipLaunchKernelGGL(fill_rows, dim3((unsigned)((arows * ld + 255) / 256)), dim3(256), 0, 0, rows, arows * ld, 1u);
+  hipLaunchKernelGGL(fill_rows, dim3((unsigned)((nqpad * ld + 255) / 256)), dim3(256), 0, 0, q, (int64_t)nqpad * ld, 7u);
+  hipLaunchKernelGGL(fill_f, dim3((unsigned)((arows + 255) / 256)), dim3(256), 0, 0, inv, arows, 1.0f);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  float best = 1e30f, tot = 0.f;
+  for (int r = 0; r < reps + 1; ++r) {
+    CK(hipMemset(tau, 0, nqpad * 4));
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL((score_topk_v3_kernel<_Float16, 512, RT, QT, WM, WN, NST>), dim3(nwg), dim3(V3_NT), 0, 0,
+                       rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, buf, tau, part, kp);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r > 0) { best = std::min(best, ms); tot += ms; }
+  }
+  const double flops = 2.0 * nqpad * N * ld, bytes = (double)N * ld * 2;
+  printf("%s nq=%d RT=%d QT=%d NST=%d: best %.3f ms avg %.3f ms  %.1f TFLOP/s  %.0f GB/s\n", name, nq, RT, QT, NST,
+         best, tot / reps, flops / (best * 1e-3) / 1e12, bytes / (best * 1e-3) / 1e9);
+  hipFree(rows); hipFree(q); hipFree(inv); hipFree(buf); hipFree(part); hipFree(tau);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  const char* name = argc > 1 ? argv[1] : "full";
+  const int64_t N = 10000000;
+  if (run<224, 256, 2, 4, 5>(name, N, 1024, 3)) return 2;
+  if (run<224, 256, 2, 4, 5>(name, N, 256, 3)) return 2;
+  if (run<256, 16, 8, 1, 8>(name, N, 16, 3)) return 2;
+  return 0;
+}
