@@ -218,6 +218,44 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
   return HCR_OK;
 }
 
+template <typename TM, int DH, int KB>
+static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+                                 hipStream_t st) {
+  const size_t lds = attention_mfma_lds<TM, DH>(S);
+  static bool attr_set = false;          // one process-wide attribute per instantiation
+  if (lds > 64 * 1024 && !attr_set) {
+    HIPC(hipFuncSetAttribute((const void*)attention_mfma_kernel<TM, DH, KB>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((attention_mfma_kernel<TM, DH, KB>), dim3((unsigned)(n * e->cfg.heads)),
+                     dim3(256), lds, st, e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden,
+                     e->cfg.heads, e->ctx.as<TM>());
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+// MFMA attention for head dims 32 / 64 up to 512 keys; the scalar kernel otherwise
+// (HCRAG_SCALAR_ATTENTION=1 forces it, for A/B checks).
+template <typename TM>
+static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+                            hipStream_t st, size_t scalar_lds) {
+  static const bool force_scalar = getenv("HCRAG_SCALAR_ATTENTION") != nullptr;
+  const int dh = e->cfg.hidden / e->cfg.heads;
+  const int Sp = (S + 31) & ~31;
+  if (!force_scalar && (dh == 32 || dh == 64) && Sp <= 512) {
+    if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, d_mask, n, S, st)
+                                   : launch_attention_mfma<TM, 32, 32>(e, d_mask, n, S, st);
+    return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, d_mask, n, S, st)
+                     : launch_attention_mfma<TM, 64, 32>(e, d_mask, n, S, st);
+  }
+  hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * e->cfg.heads)), dim3(256),
+                     scalar_lds, st, e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden,
+                     e->cfg.heads, e->ctx.as<TM>());
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 template <typename TM>
 static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask, int64_t n, int S,
                     float* d_out, hipStream_t st) {
@@ -249,9 +287,7 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
     CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
                                      L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
                                      3 * H, st)));
-    hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * NH)), dim3(256), att_lds, st,
-                       e->qkv.as<const TM>(), d_mask, S, H, NH, e->ctx.as<TM>());
-    HIPC(hipGetLastError());
+    CHECK(launch_attention<TM>(e, d_mask, n, S, st, att_lds));
     CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H, (int)T,
                                            L.bo.as<const float>(), e->x.as<const float>(), nullptr,
                                            e->y.as<float>(), H, st)));

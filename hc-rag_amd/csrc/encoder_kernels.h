@@ -235,6 +235,139 @@ attention_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, i
 }
 
 // -------------------------------------------------------------------------------------
+// MFMA self-attention for one (sequence, head), head dim DH in {32, 64}, up to 16*KB keys.
+//   Sᵀ = K·Qᵀ on 16x16x32 MFMAs (keys on the M axis): each lane ends with one query and 4
+//   keys per 16-key block, which after the softmax is exactly the A-operand layout of P·V
+//   when the contraction index is permuted as key(g, e) = 32c + 16(e >> 2) + 4g + (e & 3);
+//   V is staged transposed (Vt[c][key]) so its B operand is two 8-byte LDS reads.
+//   LDS rows are padded (K by 16, Vt by 8 elements): conflict-free fragment reads
+//   (tests/test_lds_swizzle.py).  fp32 scores / softmax / accumulation.
+// -------------------------------------------------------------------------------------
+template <typename TM, int DH, int KB>
+__global__ void __launch_bounds__(256)
+attention_mfma_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, int S, int H,
+                      int heads, TM* __restrict__ ctx) {
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  constexpr int KS = DH + 16;                 // K row stride (elements)
+  extern __shared__ __attribute__((aligned(16))) char att_mfma_sm[];
+  const int Sp = (S + 31) & ~31;
+  const int VS = Sp + 8;                      // Vt row stride (elements)
+  TM* Ks = reinterpret_cast<TM*>(att_mfma_sm);
+  TM* Vt = Ks + (size_t)Sp * KS;
+  float* Mk = reinterpret_cast<float*>(att_mfma_sm + (((size_t)Sp * KS + (size_t)DH * VS) * sizeof(TM) + 15) / 16 * 16);
+  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  const size_t row0 = (size_t)bidx * S;
+  const int ld3 = 3 * H;
+  for (int i = threadIdx.x; i < Sp * (DH / 8); i += blockDim.x) {
+    const int j = i / (DH / 8), c8 = i - j * (DH / 8);
+    uint4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+    if (j < S) {
+      const TM* base = qkv + (row0 + j) * ld3 + h * DH + c8 * 8;
+      kv = *reinterpret_cast<const uint4*>(base + H);
+      vv = *reinterpret_cast<const uint4*>(base + 2 * H);
+    }
+    *reinterpret_cast<uint4*>(Ks + (size_t)j * KS + c8 * 8) = kv;
+    const TM* ve = reinterpret_cast<const TM*>(&vv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Vt[(size_t)(c8 * 8 + e) * VS + j] = ve[e];
+  }
+  for (int j = threadIdx.x; j < Sp; j += blockDim.x)
+    Mk[j] = (j < S && mask[row0 + j]) ? 0.f : -INFINITY;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, lg = lane >> 4;
+  const int nkb = Sp / 16;
+  const float scale = rsqrtf((float)DH);
+  for (int qb = wave; qb * 16 < S; qb += blockDim.x / 64) {
+    const int qi = qb * 16 + li;
+    V qf[DH / 32];
+#pragma unroll
+    for (int kk = 0; kk < DH / 32; ++kk) {
+      if (qi < S) qf[kk] = *reinterpret_cast<const V*>(qkv + (row0 + qi) * ld3 + h * DH + kk * 32 + lg * 8);
+      else for (int e = 0; e < 8; ++e) qf[kk][e] = (TM)0.f;
+    }
+    floatx4 sc[KB];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      sc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (b < nkb) {
+#pragma unroll
+        for (int kk = 0; kk < DH / 32; ++kk) {
+          const V kf = *reinterpret_cast<const V*>(Ks + (size_t)(b * 16 + li) * KS + kk * 32 + lg * 8);
+          sc[b] = Op::run(kf, qf[kk], sc[b]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = sc[b][r] * scale + Mk[b * 16 + lg * 4 + r];
+          sc[b][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      if (b < nkb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pexp = (mx == -INFINITY) ? 0.f : __expf(sc[b][r] - mx);
+          sc[b][r] = pexp;
+          sum += pexp;
+        }
+      }
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    floatx4 o[DH / 16];
+#pragma unroll
+    for (int cb = 0; cb < DH / 16; ++cb) o[cb] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < KB / 2; ++ch) {
+      if (2 * ch < nkb) {
+        V pa;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pa[e] = (TM)sc[2 * ch][e];
+          pa[4 + e] = (TM)sc[2 * ch + 1][e];
+        }
+#pragma unroll
+        for (int cb = 0; cb < DH / 16; ++cb) {
+          const TM* vr = Vt + (size_t)(cb * 16 + li) * VS + ch * 32 + lg * 4;
+          V vb;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+          const uint2 hi = *reinterpret_cast<const uint2*>(vr + 16);
+          uint4 packed = {lo.x, lo.y, hi.x, hi.y};
+          vb = *reinterpret_cast<const V*>(&packed);
+          o[cb] = Op::run(pa, vb, o[cb]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float invr = __shfl(inv, lg * 4 + r, 64);
+      const int row = qb * 16 + lg * 4 + r;
+      if (row < S) {
+#pragma unroll
+        for (int cb = 0; cb < DH / 16; ++cb)
+          ctx[(row0 + row) * H + h * DH + cb * 16 + li] = (TM)(o[cb][r] * invr);
+      }
+    }
+  }
+}
+
+template <typename TM, int DH>
+size_t attention_mfma_lds(int S) {
+  const int Sp = (S + 31) & ~31;
+  return (((size_t)Sp * (DH + 16) + (size_t)DH * (Sp + 8)) * sizeof(TM) + 15) / 16 * 16 + (size_t)Sp * 4;
+}
+
+// -------------------------------------------------------------------------------------
 // Pooling + L2 normalise (one block per sequence).
 //   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
 //   mode 1 (CLS, bge): h_0

@@ -21,6 +21,7 @@
 #include "host_common.h"
 #include "topk_kernels.h"
 #include "score_v3.h"
+#include "score_v4.h"
 
 using namespace hcr;
 
@@ -401,12 +402,9 @@ static V3Cfg v3_cfg(int nq) {
   if (nq <= 16) return {256, 16, 8};
   if (nq <= 64) return {256, 64, 7};
   if (nq <= 128) return {256, 128, 6};
-  static const int nst_large = [] {      // HCRAG_V3_NST=3|4|5: ring depth of the large shape
-    const char* e = getenv("HCRAG_V3_NST");
-    const int v = e ? atoi(e) : 5;
-    return (v >= 3 && v <= 5) ? v : 5;
-  }();
-  return {224, 256, nst_large};
+  // large batches: v4 (256 x 256, NST 4) unless HCRAG_V3_LARGE=1 keeps v3's 224 x 256
+  static const bool v3_large = getenv("HCRAG_V3_LARGE") != nullptr;
+  return v3_large ? V3Cfg{224, 256, 5} : V3Cfg{256, 256, 4};
 }
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
@@ -429,8 +427,14 @@ static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
 
 template <typename TM, int CAP>
 static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
-  if (c.qt == 256 && c.nst == 3) launch_v3_t<TM, CAP, 224, 256, 2, 4, 3>(ix, a, st);
-  else if (c.qt == 256 && c.nst == 4) launch_v3_t<TM, CAP, 224, 256, 2, 4, 4>(ix, a, st);
+  if (c.qt == 256 && c.rt == 256)
+    hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                       ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                       ix->inv32.as<const float>(),
+                       ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                       ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                       ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                       ix->w_part.as<uint64_t>(), a.kp);
   else if (c.qt == 256) launch_v3_t<TM, CAP, 224, 256, 2, 4, 5>(ix, a, st);
   else if (c.qt == 128) launch_v3_t<TM, CAP, 256, 128, 4, 2, 6>(ix, a, st);
   else if (c.qt == 64) launch_v3_t<TM, CAP, 256, 64, 4, 2, 7>(ix, a, st);

@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
-#include "../../hc-rag_amd/csrc/score_v3.h"
+#include <vector>
+#include <algorithm>
+#include "../../hc-rag_amd/csrc/score_v4.h"
 using namespace hcr;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 2; } } while (0)
 
@@ -21,7 +23,7 @@ __global__ void fill_f(float* p, int64_t n, float v) {
 }
 
 template <int RT, int QT, int WM, int WN, int NST>
-static int run(const char* name, int64_t N, int nq, int reps) {
+static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
   const int ld = 768, kp = 64, CAP = 512;
   const int nqpad = (nq + QT - 1) / QT * QT, nqb = nqpad / QT;
   const int ntiles = (int)((N + RT - 1) / RT);
@@ -38,19 +40,40 @@ static int run(const char* name, int64_t N, int nq, int reps) {
   hipLaunchKernelGGL(fill_f, dim3((unsigned)((arows + 255) / 256)), dim3(256), 0, 0, inv, arows, 1.0f);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+#ifdef HCR_V3_STAMPS
+  uint64_t* dst; CK(hipMalloc(&dst, (size_t)nwg * 8 * 4 * 8)); CK(hipMemset(dst, 0, (size_t)nwg * 8 * 4 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(g_v3_stamps), &dst, sizeof(dst)));
+#endif
   float best = 1e30f, tot = 0.f;
   for (int r = 0; r < reps + 1; ++r) {
-    CK(hipMemset(tau, 0, nqpad * 4));
+    if (!warm || r == 0) CK(hipMemset(tau, 0, nqpad * 4));   // warm: bound left by the last run
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL((score_topk_v3_kernel<_Float16, 512, RT, QT, WM, WN, NST>), dim3(nwg), dim3(V3_NT), 0, 0,
-                       rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, buf, tau, part, kp);
+    if constexpr (WM == 0)   // v4 (256 x 256)
+      hipLaunchKernelGGL((score_topk_v4_kernel<_Float16, 512, NST>), dim3(nwg), dim3(V3_NT), 0, 0,
+                         rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
+    else
+      hipLaunchKernelGGL((score_topk_v3_kernel<_Float16, 512, RT, QT, (WM ? WM : 2), (WN ? WN : 4), NST>), dim3(nwg), dim3(V3_NT), 0, 0,
+                         rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     if (r > 0) { best = std::min(best, ms); tot += ms; }
   }
   const double flops = 2.0 * nqpad * N * ld, bytes = (double)N * ld * 2;
-  printf("%s nq=%d RT=%d QT=%d NST=%d: best %.3f ms avg %.3f ms  %.1f TFLOP/s  %.0f GB/s\n", name, nq, RT, QT, NST,
+  printf("%s%s nq=%d RT=%d QT=%d NST=%d: best %.3f ms avg %.3f ms  %.1f TFLOP/s  %.0f GB/s\n", name, warm ? "(warm bound)" : "", nq, RT, QT, NST,
          best, tot / reps, flops / (best * 1e-3) / 1e12, bytes / (best * 1e-3) / 1e9);
+#ifdef HCR_V3_STAMPS
+  {
+    std::vector<uint64_t> h((size_t)nwg * 8 * 4);
+    CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
+    double sum[4] = {0, 0, 0, 0};
+    for (size_t i = 0; i < h.size(); ++i) sum[i % 4] += (double)h[i];
+    const double all = sum[0] + sum[1] + sum[2] + sum[3];
+    printf("  stamps (share of wave cycles, last launch): epilogue %.1f%%  wait+barrier %.1f%%  issue %.1f%%  reads+mfma %.1f%%  (avg %.0f cyc per wave-step)\n",
+           100 * sum[0] / all, 100 * sum[1] / all, 100 * sum[2] / all, 100 * sum[3] / all,
+           all / (nwg * 8.0) / ((double)ntiles / P * (ld / V3_BK)));
+    hipFree(dst);
+  }
+#endif
   hipFree(rows); hipFree(q); hipFree(inv); hipFree(buf); hipFree(part); hipFree(tau);
   return 0;
 }
@@ -58,8 +81,12 @@ static int run(const char* name, int64_t N, int nq, int reps) {
 int main(int argc, char** argv) {
   const char* name = argc > 1 ? argv[1] : "full";
   const int64_t N = 10000000;
-  if (run<224, 256, 2, 4, 5>(name, N, 1024, 3)) return 2;
-  if (run<224, 256, 2, 4, 5>(name, N, 256, 3)) return 2;
-  if (run<256, 16, 8, 1, 8>(name, N, 16, 3)) return 2;
+  if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, false)) return 2;
+  if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, true)) return 2;
+  if (run<256, 256, 0, 0, 4>("v4", N, 256, 3, false)) return 2;
+  if (run<224, 256, 2, 4, 5>(name, N, 1024, 3, false)) return 2;
+  if (run<224, 256, 2, 4, 5>(name, N, 1024, 3, true)) return 2;
+  if (run<224, 256, 2, 4, 5>(name, N, 256, 3, false)) return 2;
+  if (run<256, 16, 8, 1, 8>(name, N, 16, 3, false)) return 2;
   return 0;
 }
