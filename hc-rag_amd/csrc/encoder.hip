@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "encoder_kernels.h"
+#include "gemm_v4.h"
 #include "hcrag.h"
 #include "host_common.h"
 
@@ -181,16 +182,16 @@ static int finalize_t(hcr_encoder* e) {
     std::memcpy(bqkv.data(), bq->data(), H * 4);
     std::memcpy(bqkv.data() + H, bk->data(), H * 4);
     std::memcpy(bqkv.data() + 2 * H, bv->data(), H * 4);
-    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 128), st));
-    CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 128), st));
-    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 128), st));
-    CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 128), st));
+    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 256), st));
+    CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 256), st));
+    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 256), st));
+    CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 256), st));
     CHECK(upload_f32(L.ln1g, g1->data(), H, H, st));
     CHECK(upload_f32(L.ln1b, b1->data(), H, H, st));
-    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 128), st));
-    CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 128), st));
-    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 128), st));
-    CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 128), st));
+    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 256), st));
+    CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 256), st));
+    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 256), st));
+    CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 256), st));
     CHECK(upload_f32(L.ln2g, g2->data(), H, H, st));
     CHECK(upload_f32(L.ln2b, b2->data(), H, H, st));
   }
@@ -211,6 +212,16 @@ extern "C" int hcr_encoder_finalize(hcr_encoder* e) {
 template <typename TM, int EPI>
 static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const float* bias,
                        const float* resid, TM* out_h, float* out_f, int ldo, hipStream_t st) {
+  // gfx950 path: LDS-DMA ring GEMM (gemm_v4.h); HCRAG_GEMM_V1=1 keeps the register-staged
+  // 128 x 128 kernel for A/B checks
+  static const bool v1 = getenv("HCRAG_GEMM_V1") != nullptr;
+  if (!v1 && K % V3_BK == 0) {
+    const int nft = (int)(rup(N, G4_T) / G4_T), ntt = (int)(rup(T, G4_T) / G4_T);
+    hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0,
+                       st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
+    HIPC(hipGetLastError());
+    return HCR_OK;
+  }
   const int nft = (int)(rup(N, BR) / BR), ntt = (int)(rup(T, BQ) / BQ);
   hipLaunchKernelGGL((gemm_nt_kernel<TM, EPI>), dim3((unsigned)(nft * ntt)), dim3(256), 0, st, W, X,
                      K, N, T, nft, bias, resid, out_h, out_f, ldo);
@@ -261,7 +272,7 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
                     float* d_out, hipStream_t st) {
   const auto& c = e->cfg;
   const int H = c.hidden, F = c.intermediate, NH = c.heads, dh = H / NH;
-  const int64_t T = n * (int64_t)S, Tp = rup(T, 128);
+  const int64_t T = n * (int64_t)S, Tp = rup(T, 256);
   if (T > (int64_t)1 << 30) return hcr_set_error(HCR_EINVAL, "batch too large");
   CHECK(e->x.ensure((size_t)Tp * H * 4));
   CHECK(e->y.ensure((size_t)Tp * H * 4));

@@ -1,0 +1,141 @@
+// gemm_v4.h — encoder projection GEMM on the LDS-DMA ring of the v4 score kernel
+// (score_v4.h): C[token][feature] = X[token][:] · W[feature][:] + bias (+ GELU | + residual).
+//
+// One workgroup = one 256-feature x 256-token output tile over the whole K; 8 waves (2 x 4),
+// each 128 features x 64 tokens as 8 x 4 16x16x32 MFMA blocks; K = 32 per stage, NST-stage
+// LDS-DMA ring with the 4 DMA pieces of stage s + NST - 1 interleaved between the MFMA groups
+// of stage s.  Weights as HF nn.Linear stores them ([out][in], K contiguous), rows padded to a
+// multiple of 256 with zeros; activations [Tp][K] with Tp a multiple of 256 (rows past T are
+// never written out).  Replaces the register-staged 128 x 128 gemm_nt_kernel on gfx950.
+#pragma once
+#include "encoder_kernels.h"
+#include "ring_common.h"
+
+namespace hcr {
+
+constexpr int G4_T = 256;     // features and tokens per tile
+
+template <typename TM, int EPI, int NST>
+__global__ void __launch_bounds__(V3_NT, 2)
+gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_real, int T_real,
+               int n_tiles_feat, const float* __restrict__ bias, const float* __restrict__ resid,
+               TM* __restrict__ out_h, float* __restrict__ out_f, int ldo) {
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  constexpr int STAGE = 2 * G4_T * 64;   // 32 KiB: W rows then X rows, 64 B each
+  constexpr int A_BYTES = G4_T * 64;
+  constexpr int MT = 8, NQ = 4, WN = 4, D = NST - 1;
+  __shared__ __attribute__((aligned(16))) char ring[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware: consecutive g share the token tile (X) and run on one XCD
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int ft = g % n_tiles_feat, tt = g / n_tiles_feat;
+  const int f0 = ft * G4_T, t0 = tt * G4_T;
+
+  const int ldb = K * 2;
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
+  const int voff = drow * ldb + dchunk * 16;
+  const int nsteps = K / V3_BK;
+  const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, G4_T * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(X) + (size_t)t0 * ldb), (short)0, G4_T * ldb, 0x00020000);
+  // zero-record descriptors for the tail stages (their LDS writes land in a consumed slot)
+  const __amdgpu_buffer_rsrc_t w_null = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(W), (short)0, 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_null = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(X), (short)0, 0, 0x00020000);
+
+  int is_s = 0, is_slot = 0;
+  auto issue_piece = [&](int i) {
+    const bool live = is_s < nsteps;
+    const int kofs = __builtin_amdgcn_readfirstlane(is_s * (V3_BK * 2));
+    char* sa = ring + __builtin_amdgcn_readfirstlane(is_slot) * STAGE;
+    if (i < 2) {
+      const int j = wave + 8 * i;
+      dma16(live ? w_rsrc : w_null, sa + j * 1024, voff, j * 16 * ldb + kofs);
+    } else {
+      const int j = wave + 8 * (i - 2);
+      dma16(live ? x_rsrc : x_null, sa + A_BYTES + j * 1024, voff, j * 16 * ldb + kofs);
+    }
+  };
+  auto advance = [&]() {
+    ++is_s;
+    is_slot = (is_slot + 1 == NST) ? 0 : is_slot + 1;
+  };
+  for (int i = 0; i < D; ++i) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) issue_piece(k);
+    advance();
+  }
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int fslot = v3_slot(fc, fr);
+  const int offA = (wm * 128 + fr) * 64 + fslot * 16;
+  const int offB = A_BYTES + (wn * 64 + fr) * 64 + fslot * 16;
+  floatx4 acc[MT][NQ];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  int rslot = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    v3_wait_vmcnt((D - 1) * 4);
+    v3_barrier();
+    const char* st = ring + rslot * STAGE;
+    V bq[NQ], av[MT];
+    v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int m = 2 * i; m < 2 * i + 2; ++m)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+      issue_piece(i);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NQ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    advance();
+    rslot = (rslot + 1 == NST) ? 0 : rslot + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail pieces retired before exit
+
+  // epilogue: lane holds features f..f+3 of token t for each (m, n) block
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int f = f0 + wm * 128 + m * 16 + (lane >> 4) * 4;
+    if (f >= N_real) continue;           // N_real % 4 == 0 (host-checked)
+    const float4 bb = *reinterpret_cast<const float4*>(bias + f);
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+      const int t = t0 + wn * 64 + n * 16 + (lane & 15);
+      if (t >= T_real) continue;
+      float v0 = acc[m][n][0] + bb.x, v1 = acc[m][n][1] + bb.y;
+      float v2 = acc[m][n][2] + bb.z, v3 = acc[m][n][3] + bb.w;
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+      }
+      if constexpr (EPI == EPI_BIAS_RESID) {
+        const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
+        float4 o;
+        o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
+      } else {
+        TM* o = out_h + (size_t)t * ldo + f;
+        o[0] = (TM)v0; o[1] = (TM)v1; o[2] = (TM)v2; o[3] = (TM)v3;
+      }
+    }
+  }
+}
+
+}  // namespace hcr

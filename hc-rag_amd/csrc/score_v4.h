@@ -66,35 +66,6 @@ __device__ __forceinline__ void v4_read_tile_vals(uint32_t inv_a, uint32_t tg_a,
       : "memory");
 }
 
-// the 12 MFMA fragments of a stage (8 row blocks at a, 4 query blocks at b, 1 KiB apart), one
-// wait.  Inline asm: a compiler-visible LDS read after the loop's LDS-DMA would get a
-// vmcnt(0) in front of it, draining the ring.
-template <typename V>
-__device__ __forceinline__ void v4_read_frags(uint32_t a, uint32_t b, V (&av)[8], V (&bq)[4]) {
-  asm volatile(
-      "ds_read_b128 %0, %12\n\t"
-      "ds_read_b128 %1, %12 offset:1024\n\t"
-      "ds_read_b128 %2, %12 offset:2048\n\t"
-      "ds_read_b128 %3, %12 offset:3072\n\t"
-      "ds_read_b128 %4, %12 offset:4096\n\t"
-      "ds_read_b128 %5, %12 offset:5120\n\t"
-      "ds_read_b128 %6, %12 offset:6144\n\t"
-      "ds_read_b128 %7, %12 offset:7168\n\t"
-      "ds_read_b128 %8, %13\n\t"
-      "ds_read_b128 %9, %13 offset:1024\n\t"
-      "ds_read_b128 %10, %13 offset:2048\n\t"
-      "ds_read_b128 %11, %13 offset:3072\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]),
-        "=&v"(av[6]), "=&v"(av[7]), "=&v"(bq[0]), "=&v"(bq[1]), "=&v"(bq[2]), "=&v"(bq[3])
-      : "v"(a), "v"(b)
-      : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-
 template <typename TM, int CAP, int NST>
 __global__ void __launch_bounds__(V3_NT, 2)
 score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
@@ -226,8 +197,26 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   int rslot = 0;                         // ring slot of the stage being consumed
   int ks = 0, vt = t0;
   int ep_vt = -1;                        // virtual tile whose epilogue is pending
+#ifdef HCR_V3_STAMPS
+  uint64_t st_epi = 0, st_wait = 0, st_issue = 0, st_mma = 0, ta, tb;
+#endif
   for (int s = 0; s <= nsteps; ++s) {
+#ifdef HCR_V3_STAMPS
+    V3_STAMP(ta);
+#endif
     // 1) epilogue of the tile finished by step s-1
+#ifdef HCR_V3_NO_EPI
+    if (ep_vt >= 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          if (acc[m][n][0] == 12345.f) cnt[0] = 1;
+          acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+      ep_vt = -1;
+    }
+#endif
     if (ep_vt >= 0) {
       int* prev_flag = flag + ((ep_vt + 1) & 1);
       if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
@@ -313,11 +302,17 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       ep_vt = -1;
     }
+#ifdef HCR_V3_STAMPS
+    V3_STAMP(tb); st_epi += tb - ta; ta = tb;
+#endif
     if (s == nsteps) break;
 
     // 2) stage s landed (this wave's pieces; D-1 later stages stay in flight), then everyone's
     v3_wait_vmcnt((D - 1) * 4);
     v3_barrier();
+#ifdef HCR_V3_STAMPS
+    V3_STAMP(tb); st_wait += tb - ta; ta = tb;
+#endif
 
     // 3) tile-slot pieces for the stage being issued (once per tile), then the MFMAs of stage s
     //    with the 4 pieces of stage s + D between them
@@ -327,6 +322,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       const char* st = ring + rslot * L::STAGE;
       V bq[NQ], av[MT];
       v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+#ifdef HCR_V3_STAMPS
+      V3_STAMP(tb); st_issue += tb - ta; ta = tb;
+#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -341,12 +339,21 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);       // 1 DMA piece
       }
     }
+#ifdef HCR_V3_STAMPS
+    V3_STAMP(tb); st_mma += tb - ta; ta = tb;
+#endif
     advance_cursor();
     rslot = (rslot + 1 == NST) ? 0 : rslot + 1;
     if (ks == ksteps - 1) ep_vt = vt;
     if (++ks == ksteps) { ks = 0; ++vt; }
   }
 
+#ifdef HCR_V3_STAMPS
+  if (lane == 0 && g_v3_stamps) {
+    uint64_t* o = g_v3_stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
+    o[0] = st_epi; o[1] = st_wait; o[2] = st_issue; o[3] = st_mma;
+  }
+#endif
   __syncthreads();
   for (int ql = wave; ql < QT; ql += V3_NT / 64) {
     compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,

@@ -14,6 +14,7 @@
 #pragma once
 #include "device_common.h"
 #include "tile_common.h"
+#include "ring_common.h"
 
 namespace hcr {
 
@@ -404,31 +405,6 @@ static_assert(L2_TOTAL <= 128 * 1024, "v2 LDS image must stay below 128 KiB");
 
 // LDS reads the compiler does not see: hipcc would otherwise wait vmcnt(0) for the
 // in-flight LDS-DMA of the next stage before them (a conservative alias assumption).
-__device__ __forceinline__ float4 lds_read_f4_now(const char* p) {
-  float4 v;
-  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ uint32_t lds_read_u32_now(const char* p) {
-  uint32_t v;
-  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_dst, int voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_dst, 16,
-                                           voff, soff, 0, 0);
-}
-__device__ __forceinline__ void* uniform_ptr(const void* p) {
-  const uint64_t v = (uint64_t)p;
-  // readfirstlane returns a signed int: go through uint32_t so an address whose low word has
-  // bit 31 set is not sign-extended into the high word
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-  return (void*)(((uint64_t)hi << 32) | (uint64_t)lo);
-}
-
 template <typename TM, int CAP>
 __global__ void __launch_bounds__(NT2, 2)
 score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,

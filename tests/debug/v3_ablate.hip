@@ -68,7 +68,7 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
     double sum[4] = {0, 0, 0, 0};
     for (size_t i = 0; i < h.size(); ++i) sum[i % 4] += (double)h[i];
     const double all = sum[0] + sum[1] + sum[2] + sum[3];
-    printf("  stamps (share of wave cycles, last launch): epilogue %.1f%%  wait+barrier %.1f%%  issue %.1f%%  reads+mfma %.1f%%  (avg %.0f cyc per wave-step)\n",
+    printf("  stamps (share of wave cycles, last launch): epilogue %.1f%%  wait+barrier %.1f%%  issue(v4: desc+frag reads) %.1f%%  reads+mfma(v4: mfma+dma) %.1f%%  (avg %.0f cyc per wave-step)\n",
            100 * sum[0] / all, 100 * sum[1] / all, 100 * sum[2] / all, 100 * sum[3] / all,
            all / (nwg * 8.0) / ((double)ntiles / P * (ld / V3_BK)));
     hipFree(dst);
