@@ -43,12 +43,14 @@ def parse():
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
-    p.add_argument("--cpu-queries", type=int, default=32)
+    p.add_argument("--cpu-queries", type=int, default=256)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--encoder", default="bge-base", choices=["bge-base", "minilm", "none"],
                    help="query-embedding leg: BERT shape (random init) encoded on each GPU")
     p.add_argument("--enc-seq", type=int, default=32)
     p.add_argument("--enc-steps", type=int, default=10)
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_score.json"),
+                   help="PMC HBM-traffic summary (tools/pmc_summary.py --traffic) of this config")
     p.add_argument("--sweep", default="", help="comma list of batch sizes for an extra "
                    "1-GPU sweep printed to stderr (e.g. 1,8,32,64,256,1024)")
     return p.parse_args()
@@ -81,6 +83,21 @@ def make_queries(ix_rows_fn, B, dim, dev, rank, n_local, r0):
     rows = ix_rows_fn(src_local)
     Q[: B // 2] = rows + 0.05 * torch.randn((B // 2, dim), generator=g, device=dev) / dim ** 0.5
     return Q, (src_local + r0)
+
+
+def load_traffic(path, N, D, nq, k, dtype, world):
+    """HBM bytes per score phase from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of
+    this exact config (profiles/, corrected per MI355X_MICROARCH.md §HBM), or None."""
+    try:
+        with open(path) as fh:
+            t = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    c = t.get("config", {})
+    if (c.get("rows"), c.get("dim"), c.get("batch"), c.get("k"), c.get("dtype")) != (N, D, nq, k, dtype) \
+            or world != 1:
+        return None
+    return round(t["hbm_bytes_per_search"] / 1e9, 3)
 
 
 def cpu_baseline(E_rows_f16, Q, k, n_total):
@@ -272,7 +289,10 @@ def main():
         achieved = bytes_alg / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
-    roof["kernel"] = "score_topk_kernel (fused MFMA score + top-k')"
+    roof["traffic"] = load_traffic(a.traffic_file, N, D, nq, k, a.dtype, world)
+    roof["traffic_unit"] = "GB per score phase (rocprofv3 FETCH_SIZE+WRITE_SIZE, profiles/traffic_score.json)"
+    roof["kernel"] = ("score_topk_v4_kernel (fused MFMA score + top-k'): sample pre-pass + "
+                      "dense pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
     roof["flops_per_launch"] = flops
     roof["alg_bytes_per_launch"] = bytes_alg
