@@ -43,7 +43,7 @@ def parse():
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
-    p.add_argument("--cpu-queries", type=int, default=256)
+    p.add_argument("--cpu-queries", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--encoder", default="bge-base", choices=["bge-base", "minilm", "none"],
                    help="query-embedding leg: BERT shape (random init) encoded on each GPU")

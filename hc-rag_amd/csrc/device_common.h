@@ -60,6 +60,15 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t o = shfl_xor_u64((uint64_t)__double_as_longlong(v), m);
+    v = fmax(v, __longlong_as_double((long long)o));
+  }
+  return v;
+}
+
 // ---- bitonic sort of 64*E u64 keys held E per lane (index = lane*E + e), descending ----
 // Every loop has a template-constant trip count so the network fully unrolls and v[] stays
 // in registers (a runtime index would send it to scratch).

@@ -22,6 +22,7 @@
 #include "topk_kernels.h"
 #include "score_v3.h"
 #include "score_v4.h"
+#include "score_v5.h"
 
 using namespace hcr;
 
@@ -65,6 +66,7 @@ struct hcr_index {
   bool has_mask = false;
   bool rho_dirty = true;
   double rho_host = 0.0;
+  double unit_dev_host = 1.0;   // max_r |1/inv32_r - 1| (UNIT score kernels when <= kUnitDevMax)
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
@@ -412,7 +414,20 @@ static bool v3_fits(const hcr_index* ix, V3Cfg c) {
   return (V3_NIS - 1) * (ix->ld / V3_BK) > c.nst - 1;
 }
 
-struct V3Launch { int nqb, P, nvt, tstride, kp; };
+struct V3Launch { int nqb, P, nvt, tstride, kp; bool unit; };
+
+// Largest deviation of a stored row's norm from 1, as max_r |1/inv32_r - 1| (fp64, positive
+// doubles order like their bit patterns): the certificate widening of the UNIT score kernels.
+__global__ void unit_dev_kernel(const float* __restrict__ inv32, int64_t n,
+                                unsigned long long* __restrict__ out) {
+  double m = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = fmax(m, fabs(1.0 / (double)inv32[i] - 1.0));
+  m = wave_max_f64(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
+}
+static constexpr double kUnitDevMax = 1.0 / 1024;   // UNIT kernels for L2-normalised corpora
 
 template <typename TM, int CAP, int RT, int QT, int WM, int WN, int NST>
 static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
@@ -427,7 +442,27 @@ static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
 
 template <typename TM, int CAP>
 static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
-  if (c.qt == 256 && c.rt == 256)
+  // v5 (score_v5.h) is an experiment kept for A/B: HCRAG_V5=1.  It measured ~5 % slower than
+  // v4 in situ (profiles/r01b/v5_ablation.txt); v4 stays the default.
+  static const bool use_v5 = getenv("HCRAG_V5") != nullptr;
+  if (c.qt == 256 && c.rt == 256 && use_v5) {
+    if (a.unit)
+      hipLaunchKernelGGL((score_topk_v5_kernel<TM, CAP, 4, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                         ix->inv32.as<const float>(),
+                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                         ix->w_part.as<uint64_t>(), a.kp);
+    else
+      hipLaunchKernelGGL((score_topk_v5_kernel<TM, CAP, 4, false>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                         ix->inv32.as<const float>(),
+                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                         ix->w_part.as<uint64_t>(), a.kp);
+  } else if (c.qt == 256 && c.rt == 256)
     hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                        ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
                        ix->inv32.as<const float>(),
@@ -462,7 +497,9 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>());
 }
 
-static constexpr int kSampleStride = 16;          // pre-pass samples 1 row tile in 16
+static constexpr int kSampleStrideDefault = 64;   // pre-pass samples 1 row tile in 64
+                                                  // (r01b sweep: 16 -> 64 saves ~0.6 ms at
+                                                  // 10M x 768, B = 1024)
 static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgroup has >= 32 tiles
 
 // tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
@@ -544,7 +581,10 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_cnt.ensure(16));
 
   HIPC(hipMemsetAsync(ix->w_qhat.p, 0, (size_t)nqpad * ix->ld * tms, st));
-  HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
+  // HCRAG_DEBUG_KEEP_TAUG (diagnostic only): keep the per-query bound of the previous search
+  // and skip the pre-pass -- a repeated identical batch then runs with the final bound
+  static const bool keep_taug = getenv("HCRAG_DEBUG_KEEP_TAUG") != nullptr;
+  if (!keep_taug) HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
   HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
 
   // rigorous accumulation bound: gamma_{ld+1} + 4u (u = 2^-24)
@@ -558,19 +598,36 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     float rho_f;
     memcpy(&rho_f, &rho_bits, 4);
     ix->rho_host = (double)rho_f;
+    unsigned long long* ud = reinterpret_cast<unsigned long long*>(ix->rho.as<char>() + 8);
+    HIPC(hipMemsetAsync(ud, 0, 8, ix->stream));
+    hipLaunchKernelGGL(unit_dev_kernel, dim3(1024), dim3(256), 0, ix->stream,
+                       ix->inv32.as<const float>(), ix->n, ud);
+    HIPC(hipGetLastError());
+    unsigned long long ud_bits = 0;
+    HIPC(hipStreamSynchronize(ix->stream));
+    HIPC(hipMemcpy(&ud_bits, ud, 8, hipMemcpyDeviceToHost));
+    memcpy(&ix->unit_dev_host, &ud_bits, 8);
     ix->rho_dirty = false;
   }
   const double rho = ix->rho_host;
+  // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
+  // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
+  static const bool no_unit = getenv("HCRAG_NO_UNIT") != nullptr;
+  static const bool v5_on = getenv("HCRAG_V5") != nullptr;
+  const bool unit = v5_on && !no_unit && ver == 3 && c3.rt == 256 && c3.qt == 256 &&
+                    ix->unit_dev_host <= kUnitDevMax;
+  const double unit_dev = unit ? ix->unit_dev_host : -1.0;
+  ix->stats.unit_kernel = unit ? 1 : 0;
 
   const unsigned gq = (unsigned)((nq + 3) / 4);
   if (tm_f16)
     hipLaunchKernelGGL((prep_queries_kernel<_Float16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
                        ix->ld, ix->w_qhat.as<_Float16>(), ix->w_qnorm.as<double>(),
-                       ix->w_eps.as<double>(), rho, gamma_u);
+                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev);
   else
     hipLaunchKernelGGL((prep_queries_kernel<__bf16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
                        ix->ld, ix->w_qhat.as<__bf16>(), ix->w_qnorm.as<double>(),
-                       ix->w_eps.as<double>(), rho, gamma_u);
+                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev);
   HIPC(hipGetLastError());
 
   if (ix->timing) HIPC(hipEventRecord(ix->ev0, st));
@@ -583,8 +640,12 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       const char* e = getenv("HCRAG_PREPASS_MIN_TILES");
       return e ? std::max(1, atoi(e)) : kPrepassMinTilesPerWg;
     }();
-    if (!no_prepass && ntiles >= (int64_t)P * min_tiles) {
-      V3Launch a{nqb, 0, (ntiles + kSampleStride - 1) / kSampleStride, kSampleStride, kp};
+    static const int kSampleStride = [] {   // HCRAG_SAMPLE_STRIDE: pre-pass sampling stride
+      const char* e = getenv("HCRAG_SAMPLE_STRIDE");
+      return e ? std::max(2, atoi(e)) : kSampleStrideDefault;
+    }();
+    if (!no_prepass && !keep_taug && ntiles >= (int64_t)P * min_tiles) {
+      V3Launch a{nqb, 0, (ntiles + kSampleStride - 1) / kSampleStride, kSampleStride, kp, unit};
       a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
       a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
       if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
@@ -595,7 +656,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                          sample_best, nq, kp, ix->w_taug.as<uint32_t>());
       HIPC(hipGetLastError());
     }
-    const V3Launch a{nqb, P, (int)ntiles, 1, kp};
+    const V3Launch a{nqb, P, (int)ntiles, 1, kp, unit};
     if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
     else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
   } else if (v2) {

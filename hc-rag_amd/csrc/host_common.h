@@ -33,6 +33,7 @@ struct DevBuf {
     if (p) { HIPC(hipFree(p)); p = nullptr; bytes = 0; }
     want = std::max<size_t>(want, 256);
     HIPC(hipMalloc(&p, want));
+    HIPC(hipMemset(p, 0, want));
     bytes = want;
     return HCR_OK;
   }

@@ -113,6 +113,40 @@ __device__ __forceinline__ void v4_read_frags(uint32_t a, uint32_t b, V (&av)[8]
       : "memory");
 }
 
+// Split form of v4_read_frags: issue the 4 query fragments, then the 8 row fragments, with no
+// wait; v4_frag_wait<N>(x, y) then waits until at most N of them are outstanding (LDS reads
+// complete in order) and re-defines x, y so no use of them is scheduled above the wait.
+template <typename V>
+__device__ __forceinline__ void v4_issue_frags(uint32_t a, uint32_t b, V (&av)[8], V (&bq)[4]) {
+  asm volatile(
+      "ds_read_b128 %8, %13\n\t"
+      "ds_read_b128 %9, %13 offset:1024\n\t"
+      "ds_read_b128 %10, %13 offset:2048\n\t"
+      "ds_read_b128 %11, %13 offset:3072\n\t"
+      "ds_read_b128 %0, %12\n\t"
+      "ds_read_b128 %1, %12 offset:1024\n\t"
+      "ds_read_b128 %2, %12 offset:2048\n\t"
+      "ds_read_b128 %3, %12 offset:3072\n\t"
+      "ds_read_b128 %4, %12 offset:4096\n\t"
+      "ds_read_b128 %5, %12 offset:5120\n\t"
+      "ds_read_b128 %6, %12 offset:6144\n\t"
+      "ds_read_b128 %7, %12 offset:7168"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]),
+        "=&v"(av[6]), "=&v"(av[7]), "=&v"(bq[0]), "=&v"(bq[1]), "=&v"(bq[2]), "=&v"(bq[3])
+      : "v"(a), "v"(b)
+      : "memory");
+}
+template <int N, typename V>
+__device__ __forceinline__ void v4_frag_wait(V& x, V& y) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(x), "+v"(y) : "n"(N) : "memory");
+}
+template <int N, typename V>
+__device__ __forceinline__ void v4_frag_wait6(V& x, V& y, V (&bq)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%6)"
+               : "+v"(x), "+v"(y), "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3])
+               : "n"(N) : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }

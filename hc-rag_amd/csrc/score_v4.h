@@ -321,12 +321,23 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     {
       const char* st = ring + rslot * L::STAGE;
       V bq[NQ], av[MT];
+#ifdef HCR_V4_SPLITREAD
+      // fragments land in issue order; each MFMA group waits only for its own two row blocks
+      v4_issue_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+#else
       v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+#endif
 #ifdef HCR_V3_STAMPS
       V3_STAMP(tb); st_issue += tb - ta; ta = tb;
 #endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+#ifdef HCR_V4_SPLITREAD
+        if (i == 0) v4_frag_wait6<6>(av[0], av[1], bq);
+        if (i == 1) v4_frag_wait<4>(av[2], av[3]);
+        if (i == 2) v4_frag_wait<2>(av[4], av[5]);
+        if (i == 3) v4_frag_wait<0>(av[6], av[7]);
+#endif
 #pragma unroll
         for (int m = 2 * i; m < 2 * i + 2; ++m)
 #pragma unroll

@@ -75,13 +75,14 @@ ingest_kernel(const TIN* __restrict__ in, int64_t n, int dim, int ld, int normal
 // K1: query preparation. One wave per query.
 //   q_n = q / ||q||_2 (fp64, sklearn zero rule), q^ = TM(q_n) with f16 subnormals -> 0,
 //   eps = ||q^ - q_n|| + rho*||q^|| + gamma_u*||q^||*(1+rho)   
+//         [+ the UNIT-kernel term when unit_dev >= 0]
 //   eps < 0 marks a zero query (all scores exactly 0).
 // -------------------------------------------------------------------------------------
 template <typename TM>
 __global__ void __launch_bounds__(256)
 prep_queries_kernel(const float* __restrict__ q32, int nq, int dim, int ld, TM* __restrict__ qhat,
                     double* __restrict__ qnorm, double* __restrict__ eps, double rho,
-                    double gamma_u) {
+                    double gamma_u, double unit_dev) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
@@ -110,7 +111,11 @@ prep_queries_kernel(const float* __restrict__ q32, int nq, int dim, int ld, TM* 
   if (lane == 0) {
     qnorm[q] = nr;
     const double delta = sqrt(d2), nh = sqrt(h2);
-    eps[q] = zero ? -1.0 : delta * (1.0 + 1e-9) + rho * nh + gamma_u * nh * (1.0 + rho) + 1e-12;
+    double e = delta * (1.0 + 1e-9) + rho * nh + gamma_u * nh * (1.0 + rho) + 1e-12;
+    // UNIT kernels (unit_dev >= 0): coarse = q^.e instead of fl(q^.e * inv32); the difference
+    // is <= (1 + e)(1 + 2^-24)(max_r |1/inv32_r - 1| + 2^-24)
+    if (unit_dev >= 0.0) e += (1.0 + e) * (1.0 + 0x1p-24) * (unit_dev + 0x1p-24) + 1e-15;
+    eps[q] = zero ? -1.0 : e;
   }
 }
 

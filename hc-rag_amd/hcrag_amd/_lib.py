@@ -28,7 +28,7 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("kprime", c_int32), ("widened_queries", c_int32),
                 ("uncertified_queries", c_int32), ("partitions", c_int32),
                 ("score_launches", c_int32), ("workgroups", c_int32),
-                ("score_kernel_ms", c_double)]
+                ("score_kernel_ms", c_double), ("unit_kernel", c_int32)]
 
 
 class BertConfig(ctypes.Structure):

@@ -125,6 +125,8 @@ typedef struct {
   int32_t score_launches;     /* score kernel launches timed (timing enabled only) */
   int32_t workgroups;         /* score kernel grid size of the first pass */
   double score_kernel_ms;     /* summed HIP-event time of those launches */
+  int32_t unit_kernel;        /* 1: the UNIT score kernel ran (L2-normalised corpus, raw dot
+                                 product as coarse score, widened certificate bound) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it

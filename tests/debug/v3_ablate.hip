@@ -6,7 +6,7 @@
 #include <cstdlib>
 #include <vector>
 #include <algorithm>
-#include "../../hc-rag_amd/csrc/score_v4.h"
+#include "../../hc-rag_amd/csrc/score_v5.h"
 using namespace hcr;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 2; } } while (0)
 
@@ -48,7 +48,13 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
   for (int r = 0; r < reps + 1; ++r) {
     if (!warm || r == 0) CK(hipMemset(tau, 0, nqpad * 4));   // warm: bound left by the last run
     CK(hipEventRecord(e0));
-    if constexpr (WM == 0)   // v4 (256 x 256)
+    if constexpr (WM == -1)  // v5 UNIT (256 x 256)
+      hipLaunchKernelGGL((score_topk_v5_kernel<_Float16, 512, NST, true>), dim3(nwg), dim3(V3_NT), 0, 0,
+                         rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
+    else if constexpr (WM == -2)  // v5 (256 x 256), inverse-norm path
+      hipLaunchKernelGGL((score_topk_v5_kernel<_Float16, 512, NST, false>), dim3(nwg), dim3(V3_NT), 0, 0,
+                         rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
+    else if constexpr (WM == 0)   // v4 (256 x 256)
       hipLaunchKernelGGL((score_topk_v4_kernel<_Float16, 512, NST>), dim3(nwg), dim3(V3_NT), 0, 0,
                          rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     else
@@ -58,6 +64,16 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     if (r > 0) { best = std::min(best, ms); tot += ms; }
   }
+#ifdef HCR_V5_COUNT
+  {
+    unsigned long long h[4];
+    CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_v5_count), sizeof(h)));
+    printf("  counts over %d launches: slow blocks %llu  appends %llu  epilogues %llu  compaction-epilogues %llu\n",
+           reps + 1, h[0], h[1], h[2], h[3]);
+    unsigned long long z[4] = {0, 0, 0, 0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_v5_count), z, sizeof(z)));
+  }
+#endif
   const double flops = 2.0 * nqpad * N * ld, bytes = (double)N * ld * 2;
   printf("%s%s nq=%d RT=%d QT=%d NST=%d: best %.3f ms avg %.3f ms  %.1f TFLOP/s  %.0f GB/s\n", name, warm ? "(warm bound)" : "", nq, RT, QT, NST,
          best, tot / reps, flops / (best * 1e-3) / 1e12, bytes / (best * 1e-3) / 1e9);
@@ -81,9 +97,18 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
 int main(int argc, char** argv) {
   const char* name = argc > 1 ? argv[1] : "full";
   const int64_t N = 10000000;
+#ifdef HCR_ABL_V5
+  if (run<256, 256, -1, 0, 4>("v5unit", N, 1024, 3, false)) return 2;
+  if (run<256, 256, -1, 0, 4>("v5unit", N, 1024, 3, true)) return 2;
+  if (run<256, 256, -2, 0, 4>("v5inv", N, 1024, 3, false)) return 2;
+  if (run<256, 256, -2, 0, 4>("v5inv", N, 1024, 3, true)) return 2;
+  if (run<256, 256, -1, 0, 4>("v5unit", N, 256, 3, false)) return 2;
+  return 0;
+#endif
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, false)) return 2;
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, true)) return 2;
   if (run<256, 256, 0, 0, 4>("v4", N, 256, 3, false)) return 2;
+  if (argc > 2) return 0;
   if (run<224, 256, 2, 4, 5>(name, N, 1024, 3, false)) return 2;
   if (run<224, 256, 2, 4, 5>(name, N, 1024, 3, true)) return 2;
   if (run<224, 256, 2, 4, 5>(name, N, 256, 3, false)) return 2;

@@ -371,3 +371,15 @@ def test_property_graph_store_vector_query():
     assert [n.node_id for n in got_nodes] == [f"n{i}" for i in ids[0]]
     np.testing.assert_allclose(got_scores, s[0], atol=1e-6)
     assert [n.node_id for n in gs.get(ids=["n3", "n5"])] == ["n3", "n5"]
+
+
+def test_v5_kernel_parity():
+    """The experimental v5 score kernel (opt-in HCRAG_V5=1): UNIT and inverse-norm paths,
+    row mask, widening -- in a child process because the switch is read once per process."""
+    import subprocess
+    import sys
+    env = dict(os.environ, HCRAG_V5="1", HCRAG_PREPASS_MIN_TILES="1")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "v5_check.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "v5 parity ok" in r.stdout
