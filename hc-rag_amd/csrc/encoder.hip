@@ -182,16 +182,16 @@ static int finalize_t(hcr_encoder* e) {
     std::memcpy(bqkv.data(), bq->data(), H * 4);
     std::memcpy(bqkv.data() + H, bk->data(), H * 4);
     std::memcpy(bqkv.data() + 2 * H, bv->data(), H * 4);
-    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 256), st));
-    CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 256), st));
-    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 256), st));
-    CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 256), st));
+    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 768), st));
+    CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 768), st));
+    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 768), st));
+    CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 768), st));
     CHECK(upload_f32(L.ln1g, g1->data(), H, H, st));
     CHECK(upload_f32(L.ln1b, b1->data(), H, H, st));
-    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 256), st));
-    CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 256), st));
-    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 256), st));
-    CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 256), st));
+    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 768), st));
+    CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 768), st));
+    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 768), st));
+    CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 768), st));
     CHECK(upload_f32(L.ln2g, g2->data(), H, H, st));
     CHECK(upload_f32(L.ln2b, b2->data(), H, H, st));
   }
@@ -216,9 +216,30 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
   // 128 x 128 kernel for A/B checks
   static const bool v1 = getenv("HCRAG_GEMM_V1") != nullptr;
   if (!v1 && K % V3_BK == 0) {
-    const int nft = (int)(rup(N, G4_T) / G4_T), ntt = (int)(rup(T, G4_T) / G4_T);
-    hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0,
-                       st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
+    // feature tile: 192 when it fills the last round of 256-CU workgroups better than 256
+    // (N = 768 at T = 32768: 512 tiles = 2 full rounds vs 384 = 1.5); weights are padded to
+    // a multiple of 768 rows so either tile reads whole rows.  HCRAG_GEMM_FT=256|192 forces.
+    static const int force_ft = [] {
+      const char* e = getenv("HCRAG_GEMM_FT");
+      return e ? atoi(e) : 0;
+    }();
+    const int ntt = (int)(rup(T, G4_T) / G4_T);
+    auto rounds = [&](int ft) {            // rounds of 256 resident workgroups
+      const int64_t tiles = rup(N, ft) / ft * (int64_t)ntt;
+      return (double)((tiles + 255) / 256);
+    };
+    // a 192-feature tile takes ~0.94x the time of a 256-feature one (r01c: QKV 183 vs 163 us
+    // at 6 vs 5 rounds), not 0.75x: it pays only where it removes a mostly-empty round
+    const bool ft192 = force_ft ? force_ft == 192 : (rounds(192) * 0.94 < rounds(256));
+    if (ft192) {
+      const int nft = (int)(rup(N, 192) / 192);
+      hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 192>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
+                         0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
+    } else {
+      const int nft = (int)(rup(N, G4_T) / G4_T);
+      hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 256>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
+                         0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
+    }
     HIPC(hipGetLastError());
     return HCR_OK;
   }
@@ -281,6 +302,24 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
   CHECK(e->qkv.ensure((size_t)Tp * 3 * H * sizeof(TM)));
   CHECK(e->inter.ensure((size_t)Tp * F * sizeof(TM)));
   const unsigned gT = (unsigned)((T + 3) / 4);
+  // vectorised LayerNorm kernels when H % 4 == 0 and H <= 1024 (all BERT widths here)
+  const bool ln4 = (H % 4 == 0) && H <= 1024 && !getenv("HCRAG_LN_SCALAR");
+  auto layer_norm = [&](const DevBuf& g, const DevBuf& bb) {
+    if (ln4)
+      hipLaunchKernelGGL((layernorm4_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+                         (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
+                         e->x.as<float>(), e->xh.as<TM>());
+    else
+      hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+                         (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
+                         e->x.as<float>(), e->xh.as<TM>());
+  };
+  if (ln4)
+    hipLaunchKernelGGL((embed_ln4_kernel<TM>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+                       e->wemb.as<const float>(), e->pemb.as<const float>(),
+                       e->temb.as<const float>(), e->embg.as<const float>(),
+                       e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+  else
   hipLaunchKernelGGL((embed_ln_kernel<TM>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
                      e->wemb.as<const float>(), e->pemb.as<const float>(),
                      e->temb.as<const float>(), e->embg.as<const float>(),
@@ -302,9 +341,7 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
     CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H, (int)T,
                                            L.bo.as<const float>(), e->x.as<const float>(), nullptr,
                                            e->y.as<float>(), H, st)));
-    hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
-                       (int)T, H, L.ln1g.as<const float>(), L.ln1b.as<const float>(),
-                       c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    layer_norm(L.ln1g, L.ln1b);
     HIPC(hipGetLastError());
     CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
                                           L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
@@ -312,9 +349,7 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
     CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F, H,
                                            (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
                                            nullptr, e->y.as<float>(), H, st)));
-    hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
-                       (int)T, H, L.ln2g.as<const float>(), L.ln2b.as<const float>(),
-                       c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    layer_norm(L.ln2g, L.ln2b);
     HIPC(hipGetLastError());
   }
   hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st,

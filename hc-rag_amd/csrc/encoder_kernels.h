@@ -41,6 +41,89 @@ __device__ __forceinline__ void ln_row(F val, int H, const float* __restrict__ g
   }
 }
 
+// Vectorised row LayerNorm for H % 4 == 0 and H <= 1024 (every BERT width used here): one
+// wave per row, the row held in registers as up to 4 float4 per lane (one HBM pass), float4
+// gamma/beta loads, 16-byte fp32 and 8-byte MFMA-dtype stores.  Same arithmetic as ln_row
+// (mean, then the centred second moment, rsqrtf(var + eps)).
+template <typename TM>
+__device__ __forceinline__ void ln_row4(float4 (&v)[4], int H, const float* __restrict__ g,
+                                        const float* __restrict__ b, float eps, int lane,
+                                        float* __restrict__ xo, TM* __restrict__ xho) {
+  const int H4 = H >> 2;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < H4) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  const float mean = s / H;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < H4) {
+      const float a = v[i].x - mean, c = v[i].y - mean, d = v[i].z - mean, e = v[i].w - mean;
+      q += (a * a + c * c) + (d * d + e * e);
+    }
+  for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, 64);
+  const float rstd = rsqrtf(q / H + eps);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d4 = lane + 64 * i;
+    if (d4 >= H4) continue;
+    const float4 gg = reinterpret_cast<const float4*>(g)[d4];
+    const float4 bb = reinterpret_cast<const float4*>(b)[d4];
+    float4 o;
+    o.x = (v[i].x - mean) * rstd * gg.x + bb.x;
+    o.y = (v[i].y - mean) * rstd * gg.y + bb.y;
+    o.z = (v[i].z - mean) * rstd * gg.z + bb.z;
+    o.w = (v[i].w - mean) * rstd * gg.w + bb.w;
+    reinterpret_cast<float4*>(xo)[d4] = o;
+    union { TM h[4]; uint2 u; } pk;
+    pk.h[0] = (TM)o.x; pk.h[1] = (TM)o.y; pk.h[2] = (TM)o.z; pk.h[3] = (TM)o.w;
+    reinterpret_cast<uint2*>(xho)[d4] = pk.u;
+  }
+}
+
+template <typename TM>
+__global__ void __launch_bounds__(256)
+layernorm4_kernel(const float* __restrict__ y, int T_real, int H, const float* __restrict__ g,
+                  const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T_real) return;
+  const float4* yr = reinterpret_cast<const float4*>(y + (size_t)t * H);
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (lane + 64 * i < (H >> 2)) ? yr[lane + 64 * i] : float4{0.f, 0.f, 0.f, 0.f};
+  ln_row4<TM>(v, H, g, b, eps, lane, x + (size_t)t * H, xh + (size_t)t * H);
+}
+
+template <typename TM>
+__global__ void __launch_bounds__(256)
+embed_ln4_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
+                 const float* __restrict__ wemb, const float* __restrict__ pemb,
+                 const float* __restrict__ temb, const float* __restrict__ g,
+                 const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T_real) return;
+  const float4* w = reinterpret_cast<const float4*>(wemb + (size_t)ids[t] * H);
+  const float4* p = reinterpret_cast<const float4*>(pemb + (size_t)(t % S) * H);
+  const float4* ty = reinterpret_cast<const float4*>(temb);
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int d4 = lane + 64 * i;
+    if (d4 < (H >> 2)) {
+      const float4 a = w[d4], c = p[d4], e = ty[d4];
+      v[i] = float4{a.x + c.x + e.x, a.y + c.y + e.y, a.z + c.z + e.z, a.w + c.w + e.w};
+    } else {
+      v[i] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  ln_row4<TM>(v, H, g, b, eps, lane, x + (size_t)t * H, xh + (size_t)t * H);
+}
+
 template <typename TM>
 __global__ void __launch_bounds__(256)
 embed_ln_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,

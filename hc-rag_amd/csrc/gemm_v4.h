@@ -8,6 +8,7 @@
 // multiple of 256 with zeros; activations [Tp][K] with Tp a multiple of 256 (rows past T are
 // never written out).  Replaces the register-staged 128 x 128 gemm_nt_kernel on gfx950.
 #pragma once
+#include <type_traits>
 #include "encoder_kernels.h"
 #include "ring_common.h"
 
@@ -15,16 +16,21 @@ namespace hcr {
 
 constexpr int G4_T = 256;     // features and tokens per tile
 
-template <typename TM, int EPI, int NST>
+// FT = features per tile: 256 (8 row blocks per wave) or 192 (6), the latter for N = 768 /
+// 2304 where 256-wide tiles leave the last round of workgroups half empty (1.5 and 4.5 rounds
+// of 256 CUs at T = 32768 tokens).
+template <typename TM, int EPI, int NST, int FT>
 __global__ void __launch_bounds__(V3_NT, 2)
 gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_real, int T_real,
                int n_tiles_feat, const float* __restrict__ bias, const float* __restrict__ resid,
                TM* __restrict__ out_h, float* __restrict__ out_f, int ldo) {
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
-  constexpr int STAGE = 2 * G4_T * 64;   // 32 KiB: W rows then X rows, 64 B each
-  constexpr int A_BYTES = G4_T * 64;
-  constexpr int MT = 8, NQ = 4, WN = 4, D = NST - 1;
+  static_assert(FT == 256 || FT == 192, "feature tile");
+  constexpr int STAGE = (FT + G4_T) * 64;   // W rows then X rows, 64 B each
+  constexpr int A_BYTES = FT * 64;
+  constexpr int MT = FT / 32, NQ = 4, WN = 4, D = NST - 1;
+  constexpr int NA = FT / 16, NP = NA + G4_T / 16;   // 1 KiB DMA pieces per stage
   __shared__ __attribute__((aligned(16))) char ring[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -35,7 +41,7 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int ft = g % n_tiles_feat, tt = g / n_tiles_feat;
-  const int f0 = ft * G4_T, t0 = tt * G4_T;
+  const int f0 = ft * FT, t0 = tt * G4_T;
 
   const int ldb = K * 2;
   const int drow = lane >> 2;
@@ -43,7 +49,7 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
   const int voff = drow * ldb + dchunk * 16;
   const int nsteps = K / V3_BK;
   const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, G4_T * ldb, 0x00020000);
+      uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, FT * ldb, 0x00020000);
   const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(reinterpret_cast<const char*>(X) + (size_t)t0 * ldb), (short)0, G4_T * ldb, 0x00020000);
   // zero-record descriptors for the tail stages (their LDS writes land in a consumed slot)
@@ -53,19 +59,22 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
       uniform_ptr(X), (short)0, 0, 0x00020000);
 
   int is_s = 0, is_slot = 0;
-  auto issue_piece = [&](int i) {
+  auto issue_piece = [&](int i) __attribute__((always_inline)) {
     const bool live = is_s < nsteps;
     const int kofs = __builtin_amdgcn_readfirstlane(is_s * (V3_BK * 2));
     char* sa = ring + __builtin_amdgcn_readfirstlane(is_slot) * STAGE;
-    if (i < 2) {
-      const int j = wave + 8 * i;
-      dma16(live ? w_rsrc : w_null, sa + j * 1024, voff, j * 16 * ldb + kofs);
+    // piece kinds fixed per slot i (no runtime choice between the W and X descriptors: a
+    // divergent-looking select of buffer descriptors is lowered to a stack table + waterfall):
+    // i = 0 / 3 -> W pieces wave / wave + 8 (the latter only below NA), i = 1 / 2 -> X pieces
+    if (i == 0 || i == 3) {
+      const int j = wave + (i == 3 ? 8 : 0);
+      if (i == 0 || j < NA) dma16(live ? w_rsrc : w_null, sa + j * 1024, voff, j * 16 * ldb + kofs);
     } else {
-      const int j = wave + 8 * (i - 2);
+      const int j = wave + (i == 2 ? 8 : 0);
       dma16(live ? x_rsrc : x_null, sa + A_BYTES + j * 1024, voff, j * 16 * ldb + kofs);
     }
   };
-  auto advance = [&]() {
+  auto advance = [&]() __attribute__((always_inline)) {
     ++is_s;
     is_slot = (is_slot + 1 == NST) ? 0 : is_slot + 1;
   };
@@ -77,7 +86,7 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
 
   const int fr = lane & 15, fc = lane >> 4;
   const int fslot = v3_slot(fc, fr);
-  const int offA = (wm * 128 + fr) * 64 + fslot * 16;
+  const int offA = (wm * (FT / 2) + fr) * 64 + fslot * 16;
   const int offB = A_BYTES + (wn * 64 + fr) * 64 + fslot * 16;
   floatx4 acc[MT][NQ];
 #pragma unroll
@@ -85,26 +94,48 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  const int my_pieces = (wave + 8 < NA) ? 4 : 3;   // 4 (3 for waves 4-7 at FT = 192)
   int rslot = 0;
   for (int s = 0; s < nsteps; ++s) {
-    v3_wait_vmcnt((D - 1) * 4);
+    // constant immediates only (a runtime count would become a jump table on scratch)
+    if (NP == 32 || my_pieces == 4) v3_wait_vmcnt((D - 1) * 4);
+    else v3_wait_vmcnt((D - 1) * 3);
     v3_barrier();
     const char* st = ring + rslot * STAGE;
     V bq[NQ], av[MT];
-    v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+    if constexpr (MT == 8) v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+    else v4_read_frags6<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
+    // MFMA groups between the 4 DMA pieces: row blocks [i*MT/4, (i+1)*MT/4)
+    auto group = [&](auto lo_c, auto hi_c) __attribute__((always_inline)) {
+      constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int m = 2 * i; m < 2 * i + 2; ++m)
+      for (int m = LO; m < HI; ++m)
 #pragma unroll
         for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-      issue_piece(i);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2 * NQ, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, MT / 4>;
+    using I2 = std::integral_constant<int, (2 * MT) / 4>;
+    using I3 = std::integral_constant<int, (3 * MT) / 4>;
+    using I4 = std::integral_constant<int, MT>;
+    group(I0{}, I1{});
+    issue_piece(0);
+    group(I1{}, I2{});
+    issue_piece(1);
+    group(I2{}, I3{});
+    issue_piece(2);
+    group(I3{}, I4{});
+    issue_piece(3);
+    constexpr int G0 = (MT / 4) * NQ, G1 = ((2 * MT) / 4 - MT / 4) * NQ;
+    constexpr int G2 = ((3 * MT) / 4 - (2 * MT) / 4) * NQ, G3 = (MT - (3 * MT) / 4) * NQ;
+    __builtin_amdgcn_sched_group_barrier(0x008, G0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, G1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, G2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, G3, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
     advance();
     rslot = (rslot + 1 == NST) ? 0 : rslot + 1;
   }
@@ -113,7 +144,7 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
   // epilogue: lane holds features f..f+3 of token t for each (m, n) block
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int f = f0 + wm * 128 + m * 16 + (lane >> 4) * 4;
+    const int f = f0 + wm * (FT / 2) + m * 16 + (lane >> 4) * 4;
     if (f >= N_real) continue;           // N_real % 4 == 0 (host-checked)
     const float4 bb = *reinterpret_cast<const float4*>(bias + f);
 #pragma unroll

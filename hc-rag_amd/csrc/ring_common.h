@@ -147,6 +147,27 @@ __device__ __forceinline__ void v4_frag_wait6(V& x, V& y, V (&bq)[4]) {
                : "n"(N) : "memory");
 }
 
+// 6 row-block fragments + 4 query/token fragments (gemm_v4 at 192-feature tiles), one wait
+template <typename V>
+__device__ __forceinline__ void v4_read_frags6(uint32_t a, uint32_t b, V (&av)[6], V (&bq)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %10\n\t"
+      "ds_read_b128 %1, %10 offset:1024\n\t"
+      "ds_read_b128 %2, %10 offset:2048\n\t"
+      "ds_read_b128 %3, %10 offset:3072\n\t"
+      "ds_read_b128 %4, %10 offset:4096\n\t"
+      "ds_read_b128 %5, %10 offset:5120\n\t"
+      "ds_read_b128 %6, %11\n\t"
+      "ds_read_b128 %7, %11 offset:1024\n\t"
+      "ds_read_b128 %8, %11 offset:2048\n\t"
+      "ds_read_b128 %9, %11 offset:3072\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]),
+        "=&v"(bq[0]), "=&v"(bq[1]), "=&v"(bq[2]), "=&v"(bq[3])
+      : "v"(a), "v"(b)
+      : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }

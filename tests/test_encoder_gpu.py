@@ -195,3 +195,19 @@ def test_from_pretrained_snapshot_dir(tmp_path):
     q = np.asarray(emb.get_query_embedding("t9"))
     np.testing.assert_allclose(q, got[1], atol=2e-3)
     assert emb.max_seq_length == 24 and emb.model_name == str(tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"HCRAG_GEMM_FT": "256"}, {"HCRAG_GEMM_FT": "192", "HCRAG_LN_SCALAR": "1"}])
+def test_gemm_tile_and_layernorm_variants(env):
+    """The other GEMM feature tile (256 / 192, chosen per shape by wave quantization) and the
+    scalar LayerNorm, forced through their env switches in a child process (read once)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_encoder_gpu.py"), "-m", "gpu",
+                        "-k", "tiny_ragged or minilm_shape or cls_pooling"],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
