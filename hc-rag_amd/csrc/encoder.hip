@@ -16,6 +16,7 @@
 
 #include "encoder_kernels.h"
 #include "gemm_v4.h"
+#include "gemm_p.h"
 #include "hcrag.h"
 #include "host_common.h"
 
@@ -35,7 +36,8 @@ struct hcr_encoder {
   DevBuf wemb, pemb, temb, embg, embb;
   std::vector<EncLayer> layers;
   // workspace
-  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out;
+  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out, trash;
+  int num_cus = 256;
   size_t att_lds_limit = 64 * 1024;
 };
 
@@ -64,6 +66,9 @@ extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int co
   e->device = device;
   e->cfg = c;
   e->dtype = compute_dtype;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    e->num_cus = cus;
   hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (he != hipSuccess) {
     delete e;
@@ -78,7 +83,7 @@ extern "C" int hcr_encoder_destroy(hcr_encoder* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   DevBuf* bufs[] = {&e->wemb, &e->pemb, &e->temb, &e->embg, &e->embb, &e->ids, &e->mask, &e->x,
-                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out};
+                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out, &e->trash};
   for (DevBuf* b : bufs) b->release();
   for (auto& L : e->layers) {
     DevBuf* lb[] = {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.ln1g, &L.ln1b, &L.wi, &L.bi, &L.wo2, &L.bo2, &L.ln2g, &L.ln2b};
@@ -250,6 +255,21 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
   return HCR_OK;
 }
 
+// Persistent ring GEMM (gemm_p.h): min(tiles, CUs) workgroups, each streaming a contiguous
+// share of the 256 x 256 tiles (feature tile fastest, so consecutive tiles share X).
+// EPI_BIAS_RESID writes projection + bias only (the residual is added by the LayerNorm).
+template <typename TM, int EPI>
+static int launch_gemm_p(hcr_encoder* e, const TM* W, const TM* X, int K, int N, int T,
+                         const float* bias, TM* out_h, float* out_f, int ldo, hipStream_t st) {
+  const int nft = (int)(rup(N, GP_T) / GP_T), ntt = (int)(rup(T, GP_T) / GP_T);
+  const int tiles = nft * ntt;
+  const int grid = std::min(tiles, e->num_cus);
+  hipLaunchKernelGGL((gemm_p_kernel<TM, EPI, 4>), dim3((unsigned)grid), dim3(V3_NT), 0, st, W, X,
+                     K, N, T, nft, tiles, bias, out_h, out_f, ldo, e->trash.as<float4>());
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 template <typename TM, int DH, int KB>
 static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
                                  hipStream_t st) {
@@ -332,6 +352,37 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     e->att_lds_limit = 160 * 1024;
   }
+  // persistent GEMMs + residual-adding LayerNorm: opt-in HCRAG_GEMM_P=1 (r01c: 95.7k vs
+  // 101.8k embeddings/s for the one-tile-per-workgroup GEMMs, profiles/r01c); needs K >= 64
+  static const bool use_p = getenv("HCRAG_GEMM_P") != nullptr;
+  if (use_p && ln4 && H % 32 == 0 && F % 32 == 0 && H >= 64) {
+    CHECK(e->trash.ensure(64 * 16));
+    auto ln_res = [&](const DevBuf& g, const DevBuf& bb) {
+      hipLaunchKernelGGL((layernorm4_res_kernel<TM>), dim3(gT), dim3(256), 0, st,
+                         e->y.as<const float>(), (int)T, H, g.as<const float>(),
+                         bb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    };
+    for (int l = 0; l < c.layers; ++l) {
+      const EncLayer& L = e->layers[l];
+      CHECK((launch_gemm_p<TM, EPI_BIAS>(e, L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H,
+                                         (int)T, L.bqkv.as<const float>(), e->qkv.as<TM>(), nullptr,
+                                         3 * H, st)));
+      CHECK(launch_attention<TM>(e, d_mask, n, S, st, att_lds));
+      CHECK((launch_gemm_p<TM, EPI_BIAS_RESID>(e, L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H,
+                                               (int)T, L.bo.as<const float>(), nullptr,
+                                               e->y.as<float>(), H, st)));
+      ln_res(L.ln1g, L.ln1b);
+      HIPC(hipGetLastError());
+      CHECK((launch_gemm_p<TM, EPI_BIAS_GELU>(e, L.wi.as<const TM>(), e->xh.as<const TM>(), H, F,
+                                              (int)T, L.bi.as<const float>(), e->inter.as<TM>(),
+                                              nullptr, F, st)));
+      CHECK((launch_gemm_p<TM, EPI_BIAS_RESID>(e, L.wo2.as<const TM>(), e->inter.as<const TM>(), F,
+                                               H, (int)T, L.bo2.as<const float>(), nullptr,
+                                               e->y.as<float>(), H, st)));
+      ln_res(L.ln2g, L.ln2b);
+      HIPC(hipGetLastError());
+    }
+  } else
   for (int l = 0; l < c.layers; ++l) {
     const EncLayer& L = e->layers[l];
     CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
