@@ -78,6 +78,14 @@ _SIGS = {
     "hcr_encode": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "hcr_encode_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p,
                                   c_void_p]),
+    "hcr_relevance_combine": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int, c_int64,
+                                      c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                                      c_void_p]),
+    "hcr_relevance_combine_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p,
+                                             c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                             c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -196,6 +196,49 @@ int hcr_encode(hcr_encoder* enc, const int32_t* ids, const int32_t* mask, int64_
 int hcr_encode_device(hcr_encoder* enc, const int32_t* d_ids, const int32_t* d_mask, int64_t n,
                       int S, float* d_out, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Fused non-LLM isRelevant combiners.  Replaces the per-node Python
+ * loops of experiments/isRelevant.py batch_entity_match (:300-324), batch_node_type_priority
+ * (:327-346) and batch_isRelevant's combiners (:445-501) for nq queries x nn nodes each:
+ *   semantic = (cos + 1) / 2 of cos_scores[q][j] (e.g. the exact top-k scores of hcr_search),
+ *   entity   = |Q & N| / |Q| over entity bitsets (`words` u32 per set), 0.5 / 0.1 when the
+ *              query has no entities (node has none / has some),
+ *   type     = priority[intent[q]][node_type[node]] (a [n_intents][n_types] table; the
+ *              caller maps unlisted types to the "unknown" column),
+ *   llm      = llm_scores[q][j] (NULL = 0; the reference's LLM judge is out of scope),
+ * combined per scorer (weights4 = semantic, llm, entity, type; NULL = the reference
+ * defaults 0.3 / 0.45 / 0.15 / 0.10).  node_ids[q][j] picks the node (NULL: node j; < 0: a
+ * padded slot, output -inf).  fp64, same operation order as the reference.
+ * ------------------------------------------------------------------------------------- */
+typedef enum {
+  HCR_REL_COMPOSITE = 0,
+  HCR_REL_PARALLEL = 1,
+  HCR_REL_ROUTER = 2,
+  HCR_REL_ROUTER_ALL = 3,
+  HCR_REL_ROUTER_TWO_SEM_LLM = 4,
+  HCR_REL_ROUTER_TWO_ENT_TYPE = 5,
+  HCR_REL_SINGLE_SEM = 6,
+  HCR_REL_SINGLE_LLM = 7,
+  HCR_REL_SINGLE_ENT = 8,
+  HCR_REL_SINGLE_TYPE = 9
+} hcr_rel_scorer;
+/* Host buffers, synchronous; node arrays have n_nodes entries. */
+int hcr_relevance_combine(int device, const double* cos_scores, const int64_t* node_ids,
+                          int64_t nq, int nn, int64_t n_nodes, const uint32_t* node_entity_bits,
+                          const int32_t* node_entity_count, int words,
+                          const uint32_t* query_entity_bits, const int32_t* node_type,
+                          const int32_t* query_intent, const double* priority, int n_intents,
+                          int n_types, const double* llm_scores, int scorer_type,
+                          const double* weights4, double* out);
+/* Device buffers (weights4 host), asynchronous on `stream`; no range checks. */
+int hcr_relevance_combine_device(const double* d_cos_scores, const int64_t* d_node_ids,
+                                 int64_t nq, int nn, const uint32_t* d_node_entity_bits,
+                                 const int32_t* d_node_entity_count, int words,
+                                 const uint32_t* d_query_entity_bits, const int32_t* d_node_type,
+                                 const int32_t* d_query_intent, const double* d_priority,
+                                 int n_types, const double* d_llm_scores, int scorer_type,
+                                 const double* weights4, double* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,121 @@
+"""isRelevant non-LLM metrics + combiners (experiments/isRelevant.py:197-210, 300-346,
+425-501): the oracle restatement against hand-worked answers (CPU), then the GPU kernel
+(hcr_relevance_combine) against the oracle -- bit-identical for identical cosine inputs,
+since both evaluate the reference's fp64 expressions in the reference's order."""
+import numpy as np
+import pytest
+
+from oracle import relevance as R
+
+SCORERS = ["composite", "parallel", "router", "router_all", "router_two_sem_llm",
+           "router_two_ent_type", "router_single_sem", "router_single_llm", "router_single_ent",
+           "router_single_type"]
+
+
+def test_oracle_known_answers():
+    # entity match (:311-322)
+    assert R.entity_match(["a", "b"], ["b", "c"]) == 0.5
+    assert R.entity_match(["a", "a", "b"], ["a"]) == 0.5          # sets: duplicates collapse
+    assert R.entity_match([], []) == 0.5 and R.entity_match([], ["x"]) == 0.1
+    assert R.entity_match(["red mountain bike"], ["red mountain bike", "brakes"]) == 1.0
+    # node type priority (:128-169, unknown fallback :339-342)
+    assert R.node_type_priority("product_search", "document") == 0.3
+    assert R.node_type_priority("technical_support", "specification") == 0.9
+    assert R.node_type_priority("document_request", "spaceship") == 0.1
+    # composite with the default weights (:44-47, :480-482):
+    # sem = (0.6 + 1) / 2 = 0.8 -> 0.8*0.3 + 0.5*0.45 + 0.5*0.15 + 0.3*0.10
+    s = R.combine("composite", 0.8, 0.5, 0.5, 0.3)
+    assert s == 0.8 * 0.3 + 0.5 * 0.45 + 0.5 * 0.15 + 0.3 * 0.10
+    assert abs(s - 0.57) < 1e-15
+    assert R.combine("parallel", 0.8, 0.5, 0.9, 0.3) == 0.9
+    assert R.combine("router", 0.8, 0.5, 0.9, 0.3) == (0.8 + 0.5 + 0.3) / 3
+    assert R.combine("router_two_ent_type", 0.8, 0.5, 0.9, 0.3) == (0.9 + 0.3) / 2
+    # the reference's own sample pair (input_query / input_node, :172-194), cos given
+    out = R.batch_relevance([0.6], ["red mountain bike"], "product_search",
+                            [["red mountain bike", "handlebar", "brakes", "pedals"]], ["document"],
+                            "router_two_ent_type")
+    assert out == [(1.0 + 0.3) / 2]
+
+
+def test_composite_weights_validation():
+    from hcrag_amd.relevance import CompositeWeights
+    CompositeWeights()
+    assert CompositeWeights.create_balanced().to_dict()["entity_match"] == 0.25
+    with pytest.raises(ValueError):
+        CompositeWeights(0.5, 0.5, 0.5, 0.5)
+    with pytest.raises(ValueError):
+        CompositeWeights(1.2, -0.2, 0.0, 0.0)
+
+
+def _random_case(rng, nq, nn, n_nodes):
+    vocab = [f"e{i}" for i in range(70)]
+    types = ["product", "category", "specification", "document", "annotation", "unknown",
+             "spaceship"]
+    intents = [i for i in R.PRIORITY_MATRIX]
+    node_ent = [list(rng.choice(vocab, size=rng.integers(0, 6))) for _ in range(n_nodes)]
+    node_ent[0] = []
+    node_typ = [types[i] for i in rng.integers(0, len(types), n_nodes)]
+    q_ent = [list(rng.choice(vocab, size=rng.integers(0, 4))) for _ in range(nq)]
+    q_ent[0] = []
+    q_int = [intents[i] for i in rng.integers(0, len(intents), nq)]
+    ids = rng.integers(0, n_nodes, (nq, nn)).astype(np.int64)
+    ids[1, -2:] = -1                                   # padded top-k slots
+    cos = rng.uniform(-1, 1, (nq, nn))
+    llm = rng.uniform(0, 1, (nq, nn))
+    return node_ent, node_typ, q_ent, q_int, ids, cos, llm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scorer", SCORERS)
+def test_gpu_combiners_bit_identical(scorer):
+    from hcrag_amd import relevance as G
+    rng = np.random.default_rng(SCORERS.index(scorer))
+    nq, nn, n_nodes = 9, 13, 40
+    node_ent, node_typ, q_ent, q_int, ids, cos, llm = _random_case(rng, nq, nn, n_nodes)
+    w = G.CompositeWeights(0.2, 0.3, 0.4, 0.1)
+    got = G.score_retrieved(cos, ids, q_ent, [G.QueryIntent(i) for i in q_int], node_ent,
+                            node_typ, G.ScorerType(scorer), w, llm_scores=llm)
+    for q in range(nq):
+        for j in range(nn):
+            i = ids[q, j]
+            if i < 0:
+                assert got[q, j] == -np.inf
+                continue
+            exp = R.batch_relevance([cos[q, j]], q_ent[q], q_int[q], [node_ent[i]], [node_typ[i]],
+                                    scorer, [llm[q, j]], (0.2, 0.3, 0.4, 0.1))[0]
+            assert got[q, j] == exp, (scorer, q, j, got[q, j], exp)
+
+
+@pytest.mark.gpu
+def test_batch_isrelevant_dropin():
+    """batch_isRelevant with the exact GPU cosine vs the oracle on sklearn's cosine."""
+    from sklearn.metrics.pairwise import cosine_similarity
+    from hcrag_amd import relevance as G
+    from types import SimpleNamespace as NS
+    rng = np.random.default_rng(3)
+    q = NS(text="q", embeddings=rng.random(384), entities=["red mountain bike", "x"],
+           intent=G.QueryIntent.TECHNICAL_SUPPORT)
+    nodes = [NS(text=f"n{i}", embeddings=rng.random(384), graph_relations={},
+                node_type=["document", "product", "weird"][i % 3],
+                entities=[["red mountain bike"], [], ["x", "y"]][i % 3]) for i in range(20)]
+    cos = cosine_similarity(q.embeddings.reshape(1, -1), np.stack([n.embeddings for n in nodes]))[0]
+    llm = rng.uniform(0, 1, 20)
+    for sc in G.ScorerType:
+        got = G.batch_isRelevant(q, nodes, sc, llm_scores=llm)
+        exp = R.batch_relevance(cos, q.entities, q.intent.value, [n.entities for n in nodes],
+                                [n.node_type for n in nodes], sc.value, llm)
+        # the node / query vectors are fp64 in the reference and fp32 on the device (the index's
+        # widest storage dtype): ~1e-10 in the cosine, far inside the north-star 1e-4
+        np.testing.assert_allclose(got, exp, rtol=0, atol=1e-9)
+    assert G.batch_isRelevant(q, [], G.ScorerType.COMPOSITE) == []
+    assert G.batch_entity_match(q, nodes)[:3] == [0.5, 0.0, 0.5]
+    assert G.batch_node_type_priority(q, nodes)[:3] == [1.0, 0.6, 0.1]
+    with pytest.raises(ValueError):
+        G.batch_isRelevant(q, nodes, G.ScorerType.COMPOSITE)          # needs LLM scores
+    judge_calls = []
+
+    def judge(query, batch):
+        judge_calls.append(len(batch))
+        return [0.5] * len(batch)
+    G.batch_isRelevant(q, nodes, G.ScorerType.ROUTER, batch_size=8, llm_judge=judge)
+    assert judge_calls == [8, 8, 4]                                   # isRelevant.py:523-527
