@@ -65,12 +65,12 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
     char* sa = ring + __builtin_amdgcn_readfirstlane(is_slot) * STAGE;
     // piece kinds fixed per slot i (no runtime choice between the W and X descriptors: a
     // divergent-looking select of buffer descriptors is lowered to a stack table + waterfall):
-    // i = 0 / 3 -> W pieces wave / wave + 8 (the latter only below NA), i = 1 / 2 -> X pieces
-    if (i == 0 || i == 3) {
-      const int j = wave + (i == 3 ? 8 : 0);
-      if (i == 0 || j < NA) dma16(live ? w_rsrc : w_null, sa + j * 1024, voff, j * 16 * ldb + kofs);
+    // i = 0 / 1 -> W pieces wave / wave + 8 (the latter only below NA), i = 2 / 3 -> X pieces
+    if (i < 2) {
+      const int j = wave + 8 * i;
+      if (NA == 16 || j < NA) dma16(live ? w_rsrc : w_null, sa + j * 1024, voff, j * 16 * ldb + kofs);
     } else {
-      const int j = wave + (i == 2 ? 8 : 0);
+      const int j = wave + 8 * (i - 2);
       dma16(live ? x_rsrc : x_null, sa + A_BYTES + j * 1024, voff, j * 16 * ldb + kofs);
     }
   };

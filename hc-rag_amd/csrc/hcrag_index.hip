@@ -103,11 +103,7 @@ extern "C" int hcr_index_create(int device, int dim, int dtype, int64_t capacity
     delete ix;
     return set_err(HCR_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
-  int rc = ix->rho.ensure(16);
-  if (rc == HCR_OK) {
-    hipError_t e2 = hipMemset(ix->rho.p, 0, 16);
-    if (e2 != hipSuccess) rc = set_err(HCR_EHIP, "hipMemset: %s", hipGetErrorString(e2));
-  }
+  int rc = ix->rho.ensure(16);            // zero-filled (DevBuf::ensure)
   if (rc != HCR_OK) {
     hcr_index_destroy(ix);
     return rc;
@@ -148,8 +144,10 @@ extern "C" int hcr_index_reset(hcr_index* ix) {
   ix->n = 0;
   ix->has_mask = false;
   ix->rho_dirty = true;
-  HIPC(hipMemset(ix->rho.p, 0, 16));
-  if (ix->cap > 0) HIPC(hipMemset(ix->maskbits.p, 0xFF, (size_t)((ix->cap + kSlackRows) / 32) * 4));
+  // on the index stream: a null-stream memset does not order against it
+  HIPC(hipMemsetAsync(ix->rho.p, 0, 16, ix->stream));
+  if (ix->cap > 0)
+    HIPC(hipMemsetAsync(ix->maskbits.p, 0xFF, (size_t)((ix->cap + kSlackRows) / 32) * 4, ix->stream));
   return HCR_OK;
 }
 

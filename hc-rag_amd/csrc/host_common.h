@@ -33,7 +33,11 @@ struct DevBuf {
     if (p) { HIPC(hipFree(p)); p = nullptr; bytes = 0; }
     want = std::max<size_t>(want, 256);
     HIPC(hipMalloc(&p, want));
+    // zero-fill on the null stream, then wait for it: callers use their own non-blocking
+    // streams, which do not order against the null stream (an unfinished memset would
+    // overwrite what the caller's first copy / kernel writes)
     HIPC(hipMemset(p, 0, want));
+    HIPC(hipDeviceSynchronize());
     bytes = want;
     return HCR_OK;
   }
