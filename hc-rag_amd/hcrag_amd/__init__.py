@@ -13,6 +13,7 @@ from .tokenizer import WordPieceTokenizer
 from .encoder import MINILM_L6_V2, BertEncoder, MI355XEmbedding, SentenceEmbedder, config_from_hf
 from .ingest import BatchedEmbeddingGenerator, EmbeddingStore
 from . import relevance
+from . import graph_relevance
 
 __version__ = "0.1.0"
 
@@ -20,4 +21,4 @@ __all__ = ["VectorIndex", "merge_topk_device", "EmbeddingSearch", "batch_semanti
            "WordPieceTokenizer", "BertEncoder", "SentenceEmbedder", "MI355XEmbedding", "config_from_hf",
            "MINILM_L6_V2", "device_count", "lib", "HcrError", "HCR_F16", "HCR_BF16", "HCR_F32",
            "HCR_SCORE_COSINE", "HCR_SCORE_UNIT", "BatchedEmbeddingGenerator", "EmbeddingStore",
-           "relevance"]
+           "relevance", "graph_relevance"]

@@ -46,6 +46,25 @@ class ScorerType(Enum):
     ROUTER_SINGLE_TYPE = "router_single_type"
 
 
+@dataclass
+class QueryInput:
+    """isRelevant.py:20-25."""
+    text: str
+    embeddings: np.ndarray
+    entities: List[str]
+    intent: QueryIntent
+
+
+@dataclass
+class NodeInput:
+    """isRelevant.py:28-34."""
+    text: str
+    embeddings: np.ndarray
+    graph_relations: Dict[str, Any]
+    node_type: str
+    entities: List[str]
+
+
 # hcr_rel_scorer codes (include/hcrag.h)
 _SCORER_CODE = {ScorerType.COMPOSITE: 0, ScorerType.PARALLEL: 1, ScorerType.ROUTER: 2,
                 ScorerType.ROUTER_ALL: 3, ScorerType.ROUTER_TWO_SEM_LLM: 4,
@@ -271,6 +290,6 @@ def score_retrieved(cos: np.ndarray, ids: np.ndarray, query_entities: Sequence[S
     return _combine(cos, ids, t, scorer_type, weights, llm_scores, device)
 
 
-__all__ = ["QueryIntent", "ScorerType", "CompositeWeights", "DEFAULT_COMPOSITE_WEIGHTS",
+__all__ = ["QueryIntent", "ScorerType", "QueryInput", "NodeInput", "CompositeWeights", "DEFAULT_COMPOSITE_WEIGHTS",
            "priority_matrix", "batch_semantic_similarity", "batch_entity_match",
            "batch_node_type_priority", "batch_isRelevant", "isRelevant", "score_retrieved"]
