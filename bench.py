@@ -352,6 +352,7 @@ def main():
             "encoder": enc_res,
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
                       "widened_queries": widened, "kprime": st["kprime"],
+                      "unit_kernel": st["unit_kernel"],
                       "partitions": st["partitions"], "workgroups": st["workgroups"],
                       "mfma_frac": round(flops / (avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
                       "hbm_frac_kernel": round(bytes_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

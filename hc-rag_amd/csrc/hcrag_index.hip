@@ -222,7 +222,9 @@ extern "C" int hcr_index_add_device(hcr_index* ix, const void* d_rows, int64_t n
   if (ix->n + n > (int64_t)0xFFFFFFFEll) return set_err(HCR_EINVAL, "index limited to 2^32-2 rows per shard");
   HIPC(hipSetDevice(ix->device));
   CHECK(hcr_reserve_internal(ix, ix->n + n));
-  hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+  // NULL = the legacy default stream (as every *_device entry point): the caller's work on
+  // it (e.g. torch's default stream producing the input) is ordered before ours
+  hipStream_t st = (hipStream_t)stream;
   if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
   return ingest_device(ix, d_rows, n, rows_dtype, normalize, st);
 }
@@ -460,14 +462,24 @@ static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
                          ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
                          ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
                          ix->w_part.as<uint64_t>(), a.kp);
-  } else if (c.qt == 256 && c.rt == 256)
-    hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                       ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
-                       ix->inv32.as<const float>(),
-                       ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
-                       ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
-                       ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                       ix->w_part.as<uint64_t>(), a.kp);
+  } else if (c.qt == 256 && c.rt == 256) {
+    if (a.unit)
+      hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                         ix->inv32.as<const float>(),
+                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                         ix->w_part.as<uint64_t>(), a.kp);
+    else
+      hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4, false>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                         ix->inv32.as<const float>(),
+                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+                         ix->w_part.as<uint64_t>(), a.kp);
+  }
   else if (c.qt == 256) launch_v3_t<TM, CAP, 224, 256, 2, 4, 5>(ix, a, st);
   else if (c.qt == 128) launch_v3_t<TM, CAP, 256, 128, 4, 2, 6>(ix, a, st);
   else if (c.qt == 64) launch_v3_t<TM, CAP, 256, 64, 4, 2, 7>(ix, a, st);
@@ -502,10 +514,10 @@ static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgro
 
 // tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
 __global__ void seed_tau_kernel(const uint64_t* __restrict__ merged, int nq, int kp,
-                                uint32_t* __restrict__ tau_g) {
+                                uint32_t* __restrict__ tau_g, int rank = 0) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
-  const uint64_t kth = merged[(size_t)q * kp + kp - 1];
+  const uint64_t kth = merged[(size_t)q * kp + (rank > 0 ? rank : kp) - 1];
   tau_g[q] = kth ? (uint32_t)(kth >> 32) : 0u;
 }
 
@@ -611,10 +623,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
   static const bool no_unit = getenv("HCRAG_NO_UNIT") != nullptr;
-  static const bool v5_on = getenv("HCRAG_V5") != nullptr;
-  const bool unit = v5_on && !no_unit && ver == 3 && c3.rt == 256 && c3.qt == 256 &&
+  const bool unit = !no_unit && ver == 3 && c3.rt == 256 && c3.qt == 256 &&
                     ix->unit_dev_host <= kUnitDevMax;
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
+  static const bool dbg_unit = getenv("HCRAG_DEBUG_UNIT") != nullptr;
+  if (dbg_unit)
+    fprintf(stderr, "[hcrag] unit=%d ver=%d rt=%d qt=%d unit_dev=%.3e rho=%.3e nq=%d\n", (int)unit,
+            ver, c3.rt, c3.qt, ix->unit_dev_host, rho, nq);
   ix->stats.unit_kernel = unit ? 1 : 0;
 
   const unsigned gq = (unsigned)((nq + 3) / 4);
@@ -666,6 +681,16 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
   CHECK(merge_tree(ix, nq, nqpad, P, P2, G, kp, st, &merged_ptr));
+  // HCRAG_DEBUG_ORACLE_TAU=r (diagnostic only, with HCRAG_DEBUG_KEEP_TAUG): seed the next
+  // search's bound with this search's r-th best coarse key -- the bound a perfect seeding
+  // would give, to price the dense pass's append path
+  static const int oracle_rank = [] {
+    const char* e = getenv("HCRAG_DEBUG_ORACLE_TAU");
+    return e ? atoi(e) : 0;
+  }();
+  if (oracle_rank > 0 && ver == 3)
+    hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
+                       merged_ptr, nq, kp, ix->w_taug.as<uint32_t>(), std::min(oracle_rank, kp));
 
   if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
@@ -766,7 +791,9 @@ extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t 
     return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
   if (nq > 0 && (!d_queries || !d_out_scores || !d_out_ids)) return set_err(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(ix->device));
-  hipStream_t st = stream ? (hipStream_t)stream : ix->stream;
+  // NULL = the legacy default stream (as every *_device entry point): the caller's work on
+  // it (e.g. torch's default stream producing the input) is ordered before ours
+  hipStream_t st = (hipStream_t)stream;
   if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
   return search_device_impl(ix, d_queries, nq, k, score_mode, threshold, d_out_scores, d_out_ids, st);
 }

@@ -17,6 +17,8 @@
 //    wait; the candidate-buffer bookkeeping (tau_key / cnt / flag) lives in __shared__ arrays
 //    separate from the DMA ring, so the compiler can see that it does not alias the DMA.
 #pragma once
+#include <type_traits>
+
 #include "score_v3.h"
 
 namespace hcr {
@@ -66,7 +68,10 @@ __device__ __forceinline__ void v4_read_tile_vals(uint32_t inv_a, uint32_t tg_a,
       : "memory");
 }
 
-template <typename TM, int CAP, int NST>
+// UNIT: the coarse score is the raw dot product q^.e (L2-normalised corpora; the host widens
+// eps_q by the rows' deviation from unit norm).  The epilogue of a tile with
+// neither masked nor out-of-range rows is then a max + compare on the accumulators.
+template <typename TM, int CAP, int NST, bool UNIT = false>
 __global__ void __launch_bounds__(V3_NT, 2)
 score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
@@ -217,6 +222,22 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       ep_vt = -1;
     }
 #endif
+#ifdef HCR_V4_EPI_READONLY
+    if (ep_vt >= 0) {               // ablation: tile values read + bound, no scan
+      const int slot = ep_vt % L::NIS;
+      const int lr = lane & 15, lq = lane >> 4;
+      V4TileVals tv;
+      v4_read_tile_vals(lds_addr(ring + L::INV + slot * 1024 + (wm * 128 + lq * 4) * 4),
+                        lds_addr(ring + L::TG + slot * 1024 + (wn * 64 + lr) * 4),
+                        lds_addr(ring + L::MSK + slot * 64 + wm * 16), tv);
+      if (tv.tg[0] == 12345u && tv.iv[3].x == 2.f) cnt[0] = 1;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      ep_vt = -1;
+    }
+#endif
     if (ep_vt >= 0) {
       int* prev_flag = flag + ((ep_vt + 1) & 1);
       if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
@@ -248,54 +269,71 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         const float ls = tkr[n] ? key_score(tkr[n]) : -INFINITY;
         thr[n] = fmaxf(ls, unord32(tv.tg[n]));
       }
-      // inverse norm of this lane's rows (NaN past the end / masked out)
-      float iv[MT][4];
+      // PLAIN (UNIT, no row mask, tile inside the corpus): scores are the accumulators
+      auto epi = [&](auto plain_c) __attribute__((always_inline)) {
+        constexpr bool PLAIN = decltype(plain_c)::value;
+        // inverse norm of this lane's rows (NaN past the end / masked out; 1 in UNIT mode)
+        float iv[MT][4];
+        if constexpr (!PLAIN) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const float vv[4] = {tv.iv[m].x, tv.iv[m].y, tv.iv[m].z, tv.iv[m].w};
-        const int rl = wm * 128 + m * 16 + lq * 4;
-        const uint32_t word = mask ? mw[m >> 1] : 0xFFFFFFFFu;
+          for (int m = 0; m < MT; ++m) {
+            const float vv[4] = {tv.iv[m].x, tv.iv[m].y, tv.iv[m].z, tv.iv[m].w};
+            const int rl = wm * 128 + m * 16 + lq * 4;
+            const uint32_t word = mask ? mw[m >> 1] : 0xFFFFFFFFu;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (row0 + rl + r < n_rows) && ((word >> ((rl + r) & 31)) & 1u);
-          iv[m][r] = ok ? vv[r] : __builtin_nanf("");
-        }
-      }
-      bool any = false;
-      bool hit[NQ];
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m][n][r] * iv[m][r]);
-        hit[n] = mx >= thr[n];
-        any |= hit[n];
-      }
-      if (__any(any)) {
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-          if (hit[n]) {
-            const int ql = wn * 64 + n * 16 + lr;
-#pragma unroll
-            for (int m = 0; m < MT; ++m)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float sc = acc[m][n][r] * iv[m][r];
-                if (sc >= thr[n]) {
-                  const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
-                  const uint64_t key = make_key(sc, rowl);
-                  if (key > tkr[n]) {
-                    const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-                    wbuf[(size_t)ql * CAP + pos] = key;
-                    if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
-                  }
-                }
-              }
+            for (int r = 0; r < 4; ++r) {
+              const bool ok = (row0 + rl + r < n_rows) && ((word >> ((rl + r) & 31)) & 1u);
+              iv[m][r] = ok ? (UNIT ? 1.f : vv[r]) : __builtin_nanf("");
+            }
           }
         }
-      }
+        auto score = [&](int m, int n, int r) __attribute__((always_inline)) {
+          if constexpr (PLAIN) return acc[m][n][r];
+          else return acc[m][n][r] * iv[m][r];
+        };
+        bool any = false;
+        bool hit[NQ];
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          float mx = -INFINITY;
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, score(m, n, r));
+          hit[n] = mx >= thr[n];
+          any |= hit[n];
+        }
+#ifdef HCR_V4_NO_SLOW
+        if (__any(any) && lane == 0) cnt[wave] += 1;   // ablation: fast path only
+        if (false) {
+#else
+        if (__any(any)) {
+#endif
+#pragma unroll
+          for (int n = 0; n < NQ; ++n) {
+            if (hit[n]) {
+              const int ql = wn * 64 + n * 16 + lr;
+#pragma unroll
+              for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float sc = score(m, n, r);
+                  if (sc >= thr[n]) {
+                    const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
+                    const uint64_t key = make_key(sc, rowl);
+                    if (key > tkr[n]) {
+                      const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+                      wbuf[(size_t)ql * CAP + pos] = key;
+                      if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
+                    }
+                  }
+                }
+            }
+          }
+        }
+      };
+      if (UNIT && !mask && row0 + RT <= n_rows) epi(std::true_type{});
+      else epi(std::false_type{});
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll

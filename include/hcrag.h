@@ -72,7 +72,8 @@ int hcr_index_reset(hcr_index* index);
  * Replaces DynamicEmbeddingGenerator's list append (experiments/embedding_generator.py:127)
  * + the matrix build (experiments/main.py:762). */
 int hcr_index_add(hcr_index* index, const void* rows, int64_t n, int rows_dtype, int normalize);
-/* Same from device memory, asynchronous on `stream` (hipStream_t or NULL). */
+/* Same from device memory, asynchronous on `stream` (a hipStream_t; NULL = the legacy default
+ * stream, ordered after the caller's work on it). */
 int hcr_index_add_device(hcr_index* index, const void* d_rows, int64_t n, int rows_dtype,
                          int normalize, void* stream);
 
@@ -102,7 +103,8 @@ int hcr_search(hcr_index* index, const float* queries, int64_t nq, int k, int sc
                float threshold, float* out_scores, int64_t* out_ids);
 
 /* Device variant: queries (float32, nq x dim), outputs in device memory; fp64 scores so
- * that row-sharded results merge exactly across GPUs.  Kernels run on `stream`; the call
+ * that row-sharded results merge exactly across GPUs.  Kernels run on `stream` (NULL = the
+ * legacy default stream); the call
  * synchronises that stream once per pass to read the certificate count, so
  * outputs are final when it returns. */
 int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int k,

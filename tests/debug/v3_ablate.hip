@@ -22,7 +22,7 @@ __global__ void fill_f(float* p, int64_t n, float v) {
   if (i < n) p[i] = v;
 }
 
-template <int RT, int QT, int WM, int WN, int NST>
+template <int RT, int QT, int WM, int WN, int NST, bool UNIT = false>
 static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
   const int ld = 768, kp = 64, CAP = 512;
   const int nqpad = (nq + QT - 1) / QT * QT, nqb = nqpad / QT;
@@ -55,7 +55,7 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
       hipLaunchKernelGGL((score_topk_v5_kernel<_Float16, 512, NST, false>), dim3(nwg), dim3(V3_NT), 0, 0,
                          rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     else if constexpr (WM == 0)   // v4 (256 x 256)
-      hipLaunchKernelGGL((score_topk_v4_kernel<_Float16, 512, NST>), dim3(nwg), dim3(V3_NT), 0, 0,
+      hipLaunchKernelGGL((score_topk_v4_kernel<_Float16, 512, NST, UNIT>), dim3(nwg), dim3(V3_NT), 0, 0,
                          rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     else
       hipLaunchKernelGGL((score_topk_v3_kernel<_Float16, 512, RT, QT, (WM ? WM : 2), (WN ? WN : 4), NST>), dim3(nwg), dim3(V3_NT), 0, 0,
@@ -107,6 +107,8 @@ int main(int argc, char** argv) {
 #endif
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, false)) return 2;
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, true)) return 2;
+  if (run<256, 256, 0, 0, 4, true>("v4unit", N, 1024, 3, false)) return 2;
+  if (run<256, 256, 0, 0, 4, true>("v4unit", N, 1024, 3, true)) return 2;
   if (run<256, 256, 0, 0, 4>("v4", N, 256, 3, false)) return 2;
   if (argc > 2) return 0;
   if (run<224, 256, 2, 4, 5>(name, N, 1024, 3, false)) return 2;
