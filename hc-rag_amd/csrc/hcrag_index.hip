@@ -70,7 +70,7 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt;
+      w_unc, w_cnt, w_tauest;
   hcr_search_stats stats{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -128,7 +128,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
   DevBuf* all[] = {&ix->rows, &ix->norm64, &ix->inv32, &ix->maskbits, &ix->rho,
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
-                   &ix->w_unc, &ix->w_cnt};
+                   &ix->w_unc, &ix->w_cnt, &ix->w_tauest};
   for (DevBuf* b : all) b->release();
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
   if (ix->ev1) (void)hipEventDestroy(ix->ev1);
@@ -504,21 +504,26 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
   hipLaunchKernelGGL((rescore_kernel<TS>), dim3(nq), dim3(256), lds, st, merged,
                      kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
                      ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
-                     ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>());
+                     ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
+                     ix->w_tauest.as<const uint32_t>());
 }
 
-static constexpr int kSampleStrideDefault = 64;   // pre-pass samples 1 row tile in 64
-                                                  // (r01b sweep: 16 -> 64 saves ~0.6 ms at
-                                                  // 10M x 768, B = 1024)
+static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
+                                                  // (estimated seed, r01d sweep at 10M x 768,
+                                                  // B = 1024: 64 -> 512 saves ~0.5 ms)
 static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgroup has >= 32 tiles
 
 // tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
+// rank < kp: an ESTIMATED bound (not a k'-th of any row set); it is also written to tau_est
+// so that the rescore certificate accounts for the rows it excluded
 __global__ void seed_tau_kernel(const uint64_t* __restrict__ merged, int nq, int kp,
-                                uint32_t* __restrict__ tau_g, int rank = 0) {
+                                uint32_t* __restrict__ tau_g, int rank = 0,
+                                uint32_t* __restrict__ tau_est = nullptr) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nq) return;
   const uint64_t kth = merged[(size_t)q * kp + (rank > 0 ? rank : kp) - 1];
   tau_g[q] = kth ? (uint32_t)(kth >> 32) : 0u;
+  if (tau_est) tau_est[q] = kth ? (uint32_t)(kth >> 32) : 0u;
 }
 
 // Tree merge of the per-partition lists in ix->w_part ([q][P][kp]) into one sorted top-kp list
@@ -549,7 +554,7 @@ static int merge_tree(hcr_index* ix, int nq, int nqpad, int P, int P2, int G, in
 // Returns the number of uncertified queries in *n_unc (stream is synchronised).
 static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode, double thr,
                        double* d_out_s, int64_t* d_out_i, int kp, hipStream_t st, int* n_unc,
-                       std::vector<int>* unc_list) {
+                       std::vector<int>* unc_list, bool rigorous_seed = false) {
   const uint64_t* merged_ptr = nullptr;
   // kernel choice (HCRAG_SCORE_KERNEL=v1|v2|v3 overrides): v3 (deep LDS-DMA ring, tile shape
   // by batch size) for 16-bit rows; v1 (register-staged 128 x 128, converts fp32 rows to
@@ -589,6 +594,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_merged.ensure((size_t)nqpad * std::max(P2, 1) * kp * 8 * 2));
   CHECK(ix->w_unc.ensure((size_t)nqpad * 4));
   CHECK(ix->w_cnt.ensure(16));
+  CHECK(ix->w_tauest.ensure((size_t)nqpad * 4));
 
   HIPC(hipMemsetAsync(ix->w_qhat.p, 0, (size_t)nqpad * ix->ld * tms, st));
   // HCRAG_DEBUG_KEEP_TAUG (diagnostic only): keep the per-query bound of the previous search
@@ -596,6 +602,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   static const bool keep_taug = getenv("HCRAG_DEBUG_KEEP_TAUG") != nullptr;
   if (!keep_taug) HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
   HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
+  HIPC(hipMemsetAsync(ix->w_tauest.p, 0, (size_t)nqpad * 4, st));   // 0 = no estimated bound
 
   // rigorous accumulation bound: gamma_{ld+1} + 4u (u = 2^-24)
   const double u = std::ldexp(1.0, -24);
@@ -665,8 +672,29 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
       const uint64_t* sample_best = nullptr;
       CHECK(merge_tree(ix, nq, nqpad, a.P, P2, G, kp, st, &sample_best));
+      // Seed: the sample's j-th best key.  j = k' is rigorous (k' real rows at or above it);
+      // a smaller j estimates the global k'-th best much more tightly (the sample holds
+      // lambda = k'/stride of the global top-k' on average, Poisson): j = lambda + 5 sqrt(lambda)
+      // + 3 leaves fewer than k' rows above the seed with probability ~1e-6 per query, and
+      // the certificate then counts the seed as the bound of the excluded rows, so such a
+      // query is re-run (widened, rigorous seed) instead of answered wrong.
+      // HCRAG_RIGOROUS_SEED=1 keeps j = k'; HCRAG_SEED_RANK=j forces j (tests: an aggressive
+      // seed exercises the widened certificate and the re-run)
+      static const bool rigorous_env = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
+      static const int forced_rank = [] {
+        const char* e = getenv("HCRAG_SEED_RANK");
+        return e ? std::max(1, atoi(e)) : 0;
+      }();
+      int j = kp;
+      if (!rigorous_seed && !rigorous_env) {
+        const double lam = (double)kp / kSampleStride;
+        j = forced_rank ? forced_rank
+                        : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
+        j = std::min(kp, std::max(1, j));
+      }
       hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
-                         sample_best, nq, kp, ix->w_taug.as<uint32_t>());
+                         sample_best, nq, kp, ix->w_taug.as<uint32_t>(), j,
+                         j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
       HIPC(hipGetLastError());
     }
     const V3Launch a{nqb, P, (int)ntiles, 1, kp, unit};
@@ -761,7 +789,7 @@ static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k
       std::vector<int> unc2;
       int n2 = 0;
       int rc = search_pass(ix, qsub.as<const float>(), nu, k, mode, thr, ssub.as<double>(),
-                           isub.as<int64_t>(), kp, st, &n2, &unc2);
+                           isub.as<int64_t>(), kp, st, &n2, &unc2, /*rigorous_seed=*/true);
       if (rc == HCR_OK) {
         hipLaunchKernelGGL(scatter_topk, dim3(nu), dim3(64), 0, st, ssub.as<const double>(),
                            isub.as<const int64_t>(), idx.as<const int>(), nu, k, os, oi);

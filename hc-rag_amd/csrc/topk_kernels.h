@@ -714,7 +714,7 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
                const TS* __restrict__ rows, int ld, const double* __restrict__ norm64, int k,
                int mode, double thr, int64_t id_offset, double* __restrict__ out_s,
                int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
-               int* __restrict__ unc_count) {
+               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char sm_raw[];
   double* qd = reinterpret_cast<double*>(sm_raw);
   uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
@@ -750,12 +750,15 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
   block_sort_desc_pair(hi, lo, kp);
   const int nvalid = s_nvalid;
   if (threadIdx.x == 0) {
+    // Every row outside the candidates has coarse score <= B: the k'-th candidate's coarse
+    // score when the list is full, and (estimated seed, tau_est != 0) the seed itself, below
+    // which no row was ever appended.  Without a seed a short list holds every row.
     bool cert = true;
     const double e = eps[q];
-    if (nvalid >= kp && e >= 0.0) {   // e < 0: zero query, exact scores are all 0
-      const double ckp = (double)key_score(keys[kp - 1]);
-      const double sk = unord64(hi[k - 1]);
-      cert = ckp + e < sk;
+    const uint32_t te = tau_est ? tau_est[q] : 0u;
+    if (e >= 0.0 && (nvalid >= kp || te != 0u)) {   // e < 0: zero query, exact scores all 0
+      const double b = nvalid >= kp ? (double)key_score(keys[kp - 1]) : (double)unord32(te);
+      cert = nvalid >= k && b + e < unord64(hi[k - 1]);
     }
     unc_flags[q] = cert ? 0 : 1;
     if (!cert) atomicAdd(unc_count, 1);

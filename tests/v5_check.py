@@ -1,5 +1,6 @@
-"""Parity of the experimental v5 score kernel (HCRAG_V5=1, read once per process, hence a
-subprocess of tests/test_search_gpu.py::test_v5_kernel_parity): UNIT path (L2-normalised
+"""Parity of the score kernels under process-wide switches (read once per process, hence a
+subprocess of tests/test_search_gpu.py): the experimental v5 kernel (HCRAG_V5=1), the forced
+sampling pre-pass and its estimated / aggressive seeds: UNIT path (L2-normalised
 corpus), inverse-norm path (raw corpus), row mask and k' widening, against the oracle."""
 import os
 import sys
@@ -52,7 +53,7 @@ def main():
         es, ei = O.cosine_topk(Qd, Ed.astype(np.float64), k)
         check(s, i, es, ei)
         assert ix.last_stats()["widened_queries"] > 0
-    print("v5 parity ok")
+    print("parity ok")
 
 
 if __name__ == "__main__":
