@@ -7,6 +7,7 @@
 #include <vector>
 #include <algorithm>
 #include "../../hc-rag_amd/csrc/score_v5.h"
+#include "../../hc-rag_amd/csrc/score_v6.h"
 using namespace hcr;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 2; } } while (0)
 
@@ -53,6 +54,9 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
                          rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     else if constexpr (WM == -2)  // v5 (256 x 256), inverse-norm path
       hipLaunchKernelGGL((score_topk_v5_kernel<_Float16, 512, NST, false>), dim3(nwg), dim3(V3_NT), 0, 0,
+                         rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
+    else if constexpr (WM == -3)  // v6 (256 x 256, staggered halves)
+      hipLaunchKernelGGL((score_topk_v6_kernel<_Float16, 512, NST, UNIT>), dim3(nwg), dim3(V3_NT), 0, 0,
                          rows, ld, N, ld / V3_BK, inv, nullptr, q, nqb, P, ntiles, 1, buf, tau, part, kp);
     else if constexpr (WM == 0)   // v4 (256 x 256)
       hipLaunchKernelGGL((score_topk_v4_kernel<_Float16, 512, NST, UNIT>), dim3(nwg), dim3(V3_NT), 0, 0,
@@ -104,6 +108,12 @@ int main(int argc, char** argv) {
   if (run<256, 256, -2, 0, 4>("v5inv", N, 1024, 3, true)) return 2;
   if (run<256, 256, -1, 0, 4>("v5unit", N, 256, 3, false)) return 2;
   return 0;
+#endif
+#ifdef HCR_ABL_V6
+  if (run<256, 256, -3, 0, 4>("v6", N, 1024, 3, false)) return 2;
+  if (run<256, 256, -3, 0, 4>("v6", N, 1024, 3, true)) return 2;
+  if (run<256, 256, -3, 0, 4, true>("v6unit", N, 1024, 3, false)) return 2;
+  if (run<256, 256, -3, 0, 4, true>("v6unit", N, 1024, 3, true)) return 2;
 #endif
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, false)) return 2;
   if (run<256, 256, 0, 0, 4>("v4", N, 1024, 3, true)) return 2;
