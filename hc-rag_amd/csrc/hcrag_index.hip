@@ -70,7 +70,7 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt, w_tauest;
+      w_unc, w_cnt, w_tauest, w_umax;
   hcr_search_stats stats{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -128,7 +128,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
   DevBuf* all[] = {&ix->rows, &ix->norm64, &ix->inv32, &ix->maskbits, &ix->rho,
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
-                   &ix->w_unc, &ix->w_cnt, &ix->w_tauest};
+                   &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax};
   for (DevBuf* b : all) b->release();
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
   if (ix->ev1) (void)hipEventDestroy(ix->ev1);
@@ -488,6 +488,27 @@ static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
   return HCR_OK;
 }
 
+// sampling pre-pass: v4 in MAXONLY mode, unit maxima into ix->w_umax
+template <typename TM>
+static int launch_v4_maxonly(hcr_index* ix, V3Launch a, hipStream_t st) {
+  if (a.unit)
+    hipLaunchKernelGGL((score_topk_v4_kernel<TM, 512, 4, true, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
+                       st, ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                       ix->inv32.as<const float>(),
+                       ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                       ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, a.kp);
+  else
+    hipLaunchKernelGGL((score_topk_v4_kernel<TM, 512, 4, false, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
+                       st, ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
+                       ix->inv32.as<const float>(),
+                       ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
+                       ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
+                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, a.kp);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
   switch (cap) {
@@ -511,6 +532,7 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
+static constexpr int kSampleStrideMax = 64;      // ... of the MAXONLY pre-pass (r01d)
 static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgroup has >= 32 tiles
 
 // tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
@@ -524,6 +546,27 @@ __global__ void seed_tau_kernel(const uint64_t* __restrict__ merged, int nq, int
   const uint64_t kth = merged[(size_t)q * kp + (rank > 0 ? rank : kp) - 1];
   tau_g[q] = kth ? (uint32_t)(kth >> 32) : 0u;
   if (tau_est) tau_est[q] = kth ? (uint32_t)(kth >> 32) : 0u;
+}
+
+// Seed from the sampling pre-pass's unit maxima ([U][nqpad] floats, one per 128-row half tile
+// and query): the j-th largest of a query's U maxima is the score of j distinct rows, so
+// j = k' gives a rigorous bound and a smaller j an estimate (tau_est).
+__global__ void __launch_bounds__(256)
+seed_from_maxima_kernel(const float* __restrict__ umax, int U, int nqpad, int j, int M,
+                        uint32_t* __restrict__ tau_g, uint32_t* __restrict__ tau_est) {
+  extern __shared__ uint64_t sv[];
+  const int q = blockIdx.x;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) {
+    const float v = i < U ? umax[(size_t)i * nqpad + q] : -INFINITY;
+    sv[i] = (v == v && v > -INFINITY) ? (uint64_t)ord32(v) : 0ull;   // NaN / -inf: no row
+  }
+  __syncthreads();
+  block_sort_desc_u64(sv, M);
+  if (threadIdx.x == 0) {
+    const uint32_t t = j <= U ? (uint32_t)sv[j - 1] : 0u;
+    tau_g[q] = t;
+    if (tau_est) tau_est[q] = t;
+  }
 }
 
 // Tree merge of the per-partition lists in ix->w_part ([q][P][kp]) into one sorted top-kp list
@@ -660,42 +703,63 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       const char* e = getenv("HCRAG_PREPASS_MIN_TILES");
       return e ? std::max(1, atoi(e)) : kPrepassMinTilesPerWg;
     }();
-    static const int kSampleStride = [] {   // HCRAG_SAMPLE_STRIDE: pre-pass sampling stride
+    static const int kSampleStrideEnv = [] {   // HCRAG_SAMPLE_STRIDE: pre-pass sampling stride
       const char* e = getenv("HCRAG_SAMPLE_STRIDE");
-      return e ? std::max(2, atoi(e)) : kSampleStrideDefault;
+      return e ? std::max(2, atoi(e)) : 0;
     }();
     if (!no_prepass && !keep_taug && ntiles >= (int64_t)P * min_tiles) {
-      V3Launch a{nqb, 0, (ntiles + kSampleStride - 1) / kSampleStride, kSampleStride, kp, unit};
-      a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
-      a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
-      if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
-      else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
-      const uint64_t* sample_best = nullptr;
-      CHECK(merge_tree(ix, nq, nqpad, a.P, P2, G, kp, st, &sample_best));
-      // Seed: the sample's j-th best key.  j = k' is rigorous (k' real rows at or above it);
-      // a smaller j estimates the global k'-th best much more tightly (the sample holds
-      // lambda = k'/stride of the global top-k' on average, Poisson): j = lambda + 5 sqrt(lambda)
-      // + 3 leaves fewer than k' rows above the seed with probability ~1e-6 per query, and
-      // the certificate then counts the seed as the bound of the excluded rows, so such a
-      // query is re-run (widened, rigorous seed) instead of answered wrong.
-      // HCRAG_RIGOROUS_SEED=1 keeps j = k'; HCRAG_SEED_RANK=j forces j (tests: an aggressive
-      // seed exercises the widened certificate and the re-run)
+      // Seed rank j.  j = k' is rigorous (k' real rows at or above the seed); a smaller j
+      // estimates the global k'-th best much more tightly (the sample holds lambda = k' x
+      // sampled fraction of the global top-k' on average, Poisson): j = lambda + 5 sqrt(lambda)
+      // + 3 leaves fewer than k' rows above the seed with probability ~1e-6 per query, and the
+      // certificate then counts the seed as the bound of the excluded rows, so such a query is
+      // re-run (widened, rigorous seed) instead of answered wrong.  HCRAG_RIGOROUS_SEED=1 keeps
+      // j = k'; HCRAG_SEED_RANK=j forces j (tests: an aggressive seed exercises the widened
+      // certificate and the re-run).
       static const bool rigorous_env = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
       static const int forced_rank = [] {
         const char* e = getenv("HCRAG_SEED_RANK");
         return e ? std::max(1, atoi(e)) : 0;
       }();
+      // Two pre-pass forms: MAXONLY (default for the 256 x 256 kernel: the largest score of
+      // every sampled 128-row unit per query, no candidate lists, stride 64) and the top-k'
+      // form (every sampled row a candidate, merged; stride 512; HCRAG_PREPASS_TOPK=1 or the
+      // other tile shapes).
+      static const bool topk_env = getenv("HCRAG_PREPASS_TOPK") != nullptr;
+      const bool maxonly = !topk_env && c3.rt == 256 && c3.qt == 256;
+      int stride = kSampleStrideEnv > 0 ? kSampleStrideEnv
+                                        : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
+      constexpr int kMaxUnits = 4096;
+      if (maxonly) stride = std::max<int>(stride, (int)((2 * ntiles + kMaxUnits - 1) / kMaxUnits));
+      V3Launch a{nqb, 0, (int)((ntiles + stride - 1) / stride), stride, kp, unit};
+      a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
+      a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
       int j = kp;
       if (!rigorous_seed && !rigorous_env) {
-        const double lam = (double)kp / kSampleStride;
-        j = forced_rank ? forced_rank
-                        : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
+        const double lam = (double)kp * ((double)a.nvt * tr) / (double)ix->n;
+        j = forced_rank ? forced_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
         j = std::min(kp, std::max(1, j));
       }
-      hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
-                         sample_best, nq, kp, ix->w_taug.as<uint32_t>(), j,
-                         j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
-      HIPC(hipGetLastError());
+      if (maxonly) {
+        const int U = 2 * a.nvt;
+        CHECK(ix->w_umax.ensure((size_t)U * nqpad * 4));
+        if (ix->dtype == HCR_F16) CHECK(launch_v4_maxonly<_Float16>(ix, a, st));
+        else CHECK(launch_v4_maxonly<__bf16>(ix, a, st));
+        const int M = next_pow2(U);
+        hipLaunchKernelGGL(seed_from_maxima_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 8, st,
+                           ix->w_umax.as<const float>(), U, nqpad, j, M, ix->w_taug.as<uint32_t>(),
+                           j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
+        HIPC(hipGetLastError());
+      } else {
+        if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
+        else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
+        const uint64_t* sample_best = nullptr;
+        CHECK(merge_tree(ix, nq, nqpad, a.P, P2, G, kp, st, &sample_best));
+        hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
+                           sample_best, nq, kp, ix->w_taug.as<uint32_t>(), j,
+                           j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
+        HIPC(hipGetLastError());
+      }
     }
     const V3Launch a{nqb, P, (int)ntiles, 1, kp, unit};
     if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
@@ -725,6 +789,16 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   else launch_rescore<float>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   HIPC(hipGetLastError());
 
+#ifdef HCR_V4_COUNT
+  {   // diagnostic build: v4 epilogue event counts of this pass (stderr)
+    unsigned long long h[4], z[4] = {0, 0, 0, 0};
+    HIPC(hipStreamSynchronize(st));
+    HIPC(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_v4_count), sizeof(h)));
+    HIPC(hipMemcpyToSymbol(HIP_SYMBOL(g_v4_count), z, sizeof(z)));
+    fprintf(stderr, "[v4count] nq=%d slow=%llu appends=%llu epilogues=%llu compactions=%llu\n", nq,
+            h[0], h[1], h[2], h[3]);
+  }
+#endif
   int cnt = 0;
   HIPC(hipMemcpyAsync(&cnt, ix->w_cnt.p, 4, hipMemcpyDeviceToHost, st));
   HIPC(hipStreamSynchronize(st));

@@ -25,6 +25,12 @@ namespace hcr {
 
 constexpr int V4_RT = 256, V4_QT = 256;
 
+#ifdef HCR_V4_COUNT
+// diagnostic build only: [0] slow-path entries, [1] appends (per wave), [2] epilogues (per
+// wave), [3] in-loop compactions (per workgroup)
+__device__ unsigned long long g_v4_count[4];
+#endif
+
 template <int NST>
 struct V4Layout {
   static constexpr int A_BYTES = V4_RT * 64, B_BYTES = V4_QT * 64;
@@ -71,7 +77,11 @@ __device__ __forceinline__ void v4_read_tile_vals(uint32_t inv_a, uint32_t tg_a,
 // UNIT: the coarse score is the raw dot product q^.e (L2-normalised corpora; the host widens
 // eps_q by the rows' deviation from unit norm).  The epilogue of a tile with
 // neither masked nor out-of-range rows is then a max + compare on the accumulators.
-template <typename TM, int CAP, int NST, bool UNIT = false>
+// MAXONLY: the sampling pre-pass form.  No candidates: for every 128-row half tile ("unit")
+// and query the largest coarse score goes to ((float*)buf)[(vt * 2 + wm) * nqpad + q]
+// (nqpad = nqb * 256); partials / tau_g are not touched.  The seed kernel then takes the j-th
+// largest unit maximum per query: j distinct rows at or above it.
+template <typename TM, int CAP, int NST, bool UNIT = false, bool MAXONLY = false>
 __global__ void __launch_bounds__(V3_NT, 2)
 score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
@@ -107,6 +117,7 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   if (tid == 0) { flag[0] = 0; flag[1] = 0; }
 
   if (t0 >= t1) {
+    if constexpr (MAXONLY) return;
     for (int i = tid; i < QT * kp; i += V3_NT) {
       const int ql = i / kp, j = i - ql * kp;
       partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
@@ -241,6 +252,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     if (ep_vt >= 0) {
       int* prev_flag = flag + ((ep_vt + 1) & 1);
       if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
+#ifdef HCR_V4_COUNT
+        if (tid == 0) atomicAdd(&g_v4_count[3], 1ull);
+#endif
         __syncthreads();                 // other waves' candidate stores (global) are visible
         for (int ql = wave; ql < QT; ql += V3_NT / 64) {
           if (cnt[ql] > CAP - RT)
@@ -300,14 +314,26 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
           for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int r = 0; r < 4; ++r) mx = fmaxf(mx, score(m, n, r));
+          if constexpr (MAXONLY) {
+            // lanes lq = 0..3 hold the same 16 queries over different rows
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            if (lq == 0)
+              reinterpret_cast<float*>(buf)[((size_t)ep_vt * 2 + wm) * ((size_t)nqb * QT) + qbase +
+                                            wn * 64 + n * 16 + lr] = mx;
+          }
           hit[n] = mx >= thr[n];
           any |= hit[n];
         }
+        if constexpr (MAXONLY) any = false;
 #ifdef HCR_V4_NO_SLOW
         if (__any(any) && lane == 0) cnt[wave] += 1;   // ablation: fast path only
         if (false) {
 #else
         if (__any(any)) {
+#endif
+#ifdef HCR_V4_COUNT
+          if (lane == 0) atomicAdd(&g_v4_count[0], 1ull);
 #endif
 #pragma unroll
           for (int n = 0; n < NQ; ++n) {
@@ -322,6 +348,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
                     const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
                     const uint64_t key = make_key(sc, rowl);
                     if (key > tkr[n]) {
+#ifdef HCR_V4_COUNT
+                      atomicAdd(&g_v4_count[1], 1ull);
+#endif
                       const int pos = v3_lds_add_rtn(&cnt[ql], 1);
                       wbuf[(size_t)ql * CAP + pos] = key;
                       if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
@@ -332,6 +361,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
           }
         }
       };
+#ifdef HCR_V4_COUNT
+      if (lane == 0) atomicAdd(&g_v4_count[2], 1ull);
+#endif
       if (UNIT && !mask && row0 + RT <= n_rows) epi(std::true_type{});
       else epi(std::false_type{});
 #pragma unroll
@@ -403,6 +435,7 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     o[0] = st_epi; o[1] = st_wait; o[2] = st_issue; o[3] = st_mma;
   }
 #endif
+  if constexpr (MAXONLY) return;
   __syncthreads();
   for (int ql = wave; ql < QT; ql += V3_NT / 64) {
     compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,

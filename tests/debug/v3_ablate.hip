@@ -68,6 +68,16 @@ static int run(const char* name, int64_t N, int nq, int reps, bool warm) {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     if (r > 0) { best = std::min(best, ms); tot += ms; }
   }
+#ifdef HCR_V4_COUNT
+  {
+    unsigned long long h[4];
+    CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_v4_count), sizeof(h)));
+    printf("  v4 counts over %d launches: slow entries %llu  appends %llu  epilogues %llu  compactions %llu\n",
+           reps + 1, h[0], h[1], h[2], h[3]);
+    unsigned long long z[4] = {0, 0, 0, 0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_v4_count), z, sizeof(z)));
+  }
+#endif
 #ifdef HCR_V5_COUNT
   {
     unsigned long long h[4];
