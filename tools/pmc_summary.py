@@ -61,9 +61,9 @@ def main():
         nd = 0
         for (k, c), (s, n) in agg.items():
             if a.kernel in k:
-                if c == "FETCH_SIZE":
+                if c == "FETCH_SIZE":     # the pre-pass and dense pass may be distinct names
                     tot_fetch += s
-                    nd = max(nd, n)
+                    nd += n
                 elif c == "WRITE_SIZE":
                     tot_write += s
         searches = max(nd // a.per_search, 1)
