@@ -296,6 +296,14 @@ def main():
     roof["kernel_ms_avg"] = round(avg_ms, 4)
     roof["flops_per_launch"] = flops
     roof["alg_bytes_per_launch"] = bytes_alg
+    if nq >= 384:
+        # the 256 x 256 kernel's LDS fill: every stage brings 256 rows + 256 queries x 32 k
+        # by LDS-DMA for 2*256*256*32 flop (128 flop per byte); the dense pass's rate of it
+        # (the fill, not the MFMA pipe, bounds this tiling)
+        n_tiles = -(-nloc // 256)
+        fill = n_tiles * (-(-nq // 256)) * 512 * D * elt
+        roof["lds_dma_fill_bytes"] = fill
+        roof["lds_dma_fill_TBps"] = round(fill / (avg_ms * 1e-3) / 1e12, 2)
 
     value = nq / (elapsed / a.steps)
     cpu = None

@@ -176,8 +176,10 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       const int j = wave + 8 * i;
       dma16(d.a, d.sa + j * 1024, voff, j * 16 * ldb + d.kofs);
     } else {
+#ifndef HCR_V4_NO_QDMA     // ablation: the query half of every stage not refilled (timing only)
       const int j = wave + 8 * (i - 2);
       dma16(d.q, d.sa + L::A_BYTES + j * 1024, voff, j * 16 * ldb + d.kofs);
+#endif
     }
   };
   auto advance_cursor = [&]() {
@@ -378,7 +380,11 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     if (s == nsteps) break;
 
     // 2) stage s landed (this wave's pieces; D-1 later stages stay in flight), then everyone's
+#ifdef HCR_V4_NO_QDMA
+    v3_wait_vmcnt((D - 1) * 2);
+#else
     v3_wait_vmcnt((D - 1) * 4);
+#endif
     v3_barrier();
 #ifdef HCR_V3_STAMPS
     V3_STAMP(tb); st_wait += tb - ta; ta = tb;
