@@ -444,8 +444,14 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   if constexpr (MAXONLY) return;
   __syncthreads();
   for (int ql = wave; ql < QT; ql += V3_NT / 64) {
+    uint64_t* out = partials + ((size_t)(qbase + ql) * P + p) * kp;
+    const int c = cnt[ql];
+    if (c <= kp) {             // the list already fits: copy (the merge sorts), zero the rest
+      for (int i = lane; i < kp; i += 64) out[i] = i < c ? wbuf[(size_t)ql * CAP + i] : 0ull;
+      continue;
+    }
     compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
-                           lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
+                           lane, out);
   }
 }
 
