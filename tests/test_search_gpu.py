@@ -390,7 +390,9 @@ def test_v5_kernel_parity():
     {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_RIGOROUS_SEED": "1"},
     # aggressive seed (the sample's best row): short candidate lists, the seed-aware
     # certificate and the rigorous re-run of what it cannot certify
-    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_SAMPLE_STRIDE": "2", "HCRAG_SEED_RANK": "1"}])
+    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_SAMPLE_STRIDE": "2", "HCRAG_SEED_RANK": "1"},
+    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_TEST_DTYPE": "bf16"},
+    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_PREPASS_TOPK": "1"}])         # the top-k' pre-pass form
 def test_prepass_seed_parity(env):
     """The sampling pre-pass forced on small corpora: ids identical to the oracle whatever the
     seed, certificates complete after widening."""

@@ -21,13 +21,14 @@ def check(s, i, es, ei):
 
 
 def main():
+    dt = os.environ.get("HCRAG_TEST_DTYPE", "f16")      # storage dtype of the indexes
     rng = np.random.default_rng(5)
     N, D, B, k = 40000, 256, 512, 32
     E = rng.standard_normal((N, D)).astype(np.float32)
     Q = rng.standard_normal((B, D)).astype(np.float32)
     Q[: B // 2] = E[rng.integers(0, N, B // 2)] + 0.1 * rng.standard_normal((B // 2, D)).astype(np.float32)
     for normalize, want_unit in ((True, 1), (False, 0)):
-        with hc.VectorIndex(D, "f16") as ix:
+        with hc.VectorIndex(D, dt) as ix:
             ix.add(E, normalize=normalize)
             R = ix.get_rows()
             s, i = ix.search(Q, k)
@@ -47,10 +48,10 @@ def main():
     Ed[dup] = Ed[dup[0]]
     Qd = rng.standard_normal((B, D)).astype(np.float32)
     Qd[:8] = Ed[dup[0]].astype(np.float32)
-    with hc.VectorIndex(D, "f16") as ix:
+    with hc.VectorIndex(D, dt) as ix:
         ix.add(Ed, normalize=False)
         s, i = ix.search(Qd, k)
-        es, ei = O.cosine_topk(Qd, Ed.astype(np.float64), k)
+        es, ei = O.cosine_topk(Qd, ix.get_rows().astype(np.float64), k)
         check(s, i, es, ei)
         assert ix.last_stats()["widened_queries"] > 0
     print("parity ok")
