@@ -219,6 +219,47 @@ def test_device_api_and_shard_merge(hc):
     _check(out_s.cpu().numpy(), out_i.cpu().numpy(), es, ei, tol=SCORE_TOL_F64)
 
 
+@pytest.mark.parametrize("W", [2, 8])
+def test_rank_shapes_of_the_scaling_bench(hc, W):
+    """The local search each rank of ``bench.py --gpus W`` runs: nq = W x B gathered queries
+    (8192 at W = 8) over a row shard, through the same hip_local_search / hip_merge callables
+    ShardedSearch uses; the W shards run one after another on one GPU, the all-to-all is the
+    slice [j*B:(j+1)*B] of shard r's result, and the merged lists must equal the unsharded
+    oracle exactly."""
+    torch = pytest.importorskip("torch")
+    from hcrag_amd.distributed import shard_range, hip_local_search, hip_merge
+    rng = np.random.default_rng(100 + W)
+    D, N, B, k = 768, 12000, 1024, 32
+    E = rng.standard_normal((N, D)).astype(np.float16)
+    Q = rng.standard_normal((W * B, D)).astype(np.float32)
+    planted = rng.integers(0, N, W * B // 2)
+    Q[::2] = E[planted] + 0.1 * rng.standard_normal((W * B // 2, D))
+    dev = torch.device("cuda:0")
+    q_all = torch.from_numpy(Q).to(dev)
+    S = torch.empty((W, W * B, k), dtype=torch.float64, device=dev)
+    I = torch.empty((W, W * B, k), dtype=torch.int64, device=dev)
+    for r in range(W):
+        r0, r1 = shard_range(N, r, W)
+        with hc.VectorIndex(D, "f16", capacity=r1 - r0) as ix:
+            ix.add(E[r0:r1], normalize=False)
+            ix.set_id_offset(r0)
+            s, i = hip_local_search(ix, k)(q_all)
+            torch.cuda.synchronize()
+            assert ix.last_stats()["uncertified_queries"] == 0
+            S[r], I[r] = s, i
+    merge = hip_merge(k)
+    sub = np.r_[0:64, B - 32:B + 32, W * B - 64:W * B]      # first, a rank boundary, last
+    es, ei = O.cosine_topk(Q[sub], E.astype(np.float64), k)
+    got_s = np.empty((W * B, k)); got_i = np.empty((W * B, k), dtype=np.int64)
+    for j in range(W):                   # rank j receives block j of every shard's result
+        ms, mi = merge(S[:, j * B:(j + 1) * B].contiguous(), I[:, j * B:(j + 1) * B].contiguous())
+        torch.cuda.synchronize()
+        got_s[j * B:(j + 1) * B], got_i[j * B:(j + 1) * B] = ms.cpu().numpy(), mi.cpu().numpy()
+    _check(got_s[sub], got_i[sub], es, ei, tol=SCORE_TOL_F64)
+    # planted queries find their own row first
+    assert np.mean(got_i[::2, 0] == planted) > 0.99
+
+
 def test_embedding_search_dropin(hc):
     rng = np.random.default_rng(13)
     M = rng.standard_normal((441, 384))            # config 1 scale (Product*.csv rows)
