@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--encoder", default="bge-base", choices=["bge-base", "minilm", "none"],
+    p.add_argument("--encoder", default="bge-base", choices=["bge-base", "bge-large", "minilm", "none"],
                    help="query-embedding leg: BERT shape (random init) encoded on each GPU")
     p.add_argument("--enc-seq", type=int, default=32)
     p.add_argument("--enc-steps", type=int, default=10)
@@ -83,6 +83,14 @@ def make_queries(ix_rows_fn, B, dim, dev, rank, n_local, r0):
     rows = ix_rows_fn(src_local)
     Q[: B // 2] = rows + 0.05 * torch.randn((B // 2, dim), generator=g, device=dev) / dim ** 0.5
     return Q, (src_local + r0)
+
+
+def workload_name(N, D, dtype, B, k, world):
+    """Names the BASELINE.json config a run matches (configs[2] is the default headline)."""
+    tag = {(10_000_000, 768, 1024, 32): "configs[2]", (1_000_000, 384, 256, 10): "configs[1]",
+           (100_000_000 // 8, 1024, 1024, 64): "configs[4] per-rank shape"}.get((N, D, B, k), "custom")
+    return (f"{tag}: {N:,} x {D} {dtype} node embeddings, batch={B} queries per GPU, top-{k} "
+            f"(row-sharded over {world} GPU{'s' if world > 1 else ''})")
 
 
 def load_traffic(path, N, D, nq, k, dtype, world):
@@ -126,6 +134,9 @@ ENC_SHAPES = {
     # bge-base-en (768-d, the corpus dim of configs[2]; CLS pooling) and all-MiniLM-L6-v2
     "bge-base": dict(vocab_size=30522, hidden=768, layers=12, heads=12, intermediate=3072,
                      max_position=512, type_vocab=2, layer_norm_eps=1e-12, pooling=1, normalize=1),
+    # bge-large-en (1024-d, the corpus dim of configs[4])
+    "bge-large": dict(vocab_size=30522, hidden=1024, layers=24, heads=16, intermediate=4096,
+                      max_position=512, type_vocab=2, layer_norm_eps=1e-12, pooling=1, normalize=1),
     "minilm": dict(vocab_size=30522, hidden=384, layers=6, heads=12, intermediate=1536,
                    max_position=512, type_vocab=2, layer_norm_eps=1e-12, pooling=0, normalize=1),
 }
@@ -351,8 +362,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic: N(0,1) rows L2-normalised at ingest then rounded to fp16; "
                     "queries 50% planted (corpus row + noise) / 50% random, fp32, HBM-resident",
-            "config": {"workload": "configs[2]: 10M x 768 fp16 node embeddings, batch=1024 "
-                                   "queries per GPU, top-32 (row-sharded over GPUs)",
+            "config": {"workload": workload_name(N, D, a.dtype, B, k, world),
                        "rows": N, "dim": D, "batch_per_gpu": B, "global_batch": nq, "k": k,
                        "parallelism": f"rowshard{world}" + ("+rccl_allgather_alltoall" if world > 1 else "")},
             "roofline": roof,

@@ -533,7 +533,9 @@ static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
 static constexpr int kSampleStrideMax = 64;      // ... of the MAXONLY pre-pass (r01d)
-static constexpr int kPrepassMinTilesPerWg = 32;  // ... when each dense workgroup has >= 32 tiles
+static constexpr int kPrepassMinTilesPerWg = 4;   // ... when each dense workgroup has >= 4 tiles
+                                                  // (r01g, configs[1] 1M x 384 B = 256: 15 tiles
+                                                  // per workgroup; seeded 0.32 ms vs cold 1.84 ms)
 
 // tau_g[q] = ord32 score of the k'-th best key of the sample's merged list (0 if short)
 // rank < kp: an ESTIMATED bound (not a k'-th of any row set); it is also written to tau_est

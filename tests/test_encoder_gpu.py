@@ -98,6 +98,27 @@ def test_minilm_shape(dtype):
     _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask), dtype)
 
 
+BGE_BASE_2L = dict(vocab_size=30522, hidden_size=768, num_hidden_layers=2, num_attention_heads=12,
+                   intermediate_size=3072, max_position_embeddings=512, type_vocab_size=2)
+BGE_LARGE_2L = dict(vocab_size=30522, hidden_size=1024, num_hidden_layers=2, num_attention_heads=16,
+                    intermediate_size=4096, max_position_embeddings=512, type_vocab_size=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["bge-base", "bge-large"])
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_bge_shapes_cls(shape, dtype):
+    """The corpus encoders of configs[2] (768-d) and configs[4] (1024-d, 16 heads, FFN 4096),
+    2 of their layers, CLS pooling + L2 as the bge models use: every GEMM shape of both
+    (N = 768/2304/3072 and 1024/3072/4096) on the LDS-DMA GEMM, ragged lengths."""
+    cfg = BGE_BASE_2L if shape == "bge-base" else BGE_LARGE_2L
+    conf, m = _hf_model(cfg, 5)
+    rng = np.random.default_rng(5)
+    ids, mask = _batch(rng, 40, 64, cfg["vocab_size"])
+    enc = _encoder(conf, m, dtype, pooling="cls")
+    _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask, "cls"), dtype)
+
+
 @pytest.mark.gpu
 def test_cls_pooling_and_no_normalize():
     conf, m = _hf_model(TINY, 3)

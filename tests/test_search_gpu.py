@@ -433,7 +433,8 @@ def test_v5_kernel_parity():
     # certificate and the rigorous re-run of what it cannot certify
     {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_SAMPLE_STRIDE": "2", "HCRAG_SEED_RANK": "1"},
     {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_TEST_DTYPE": "bf16"},
-    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_PREPASS_TOPK": "1"}])         # the top-k' pre-pass form
+    {"HCRAG_PREPASS_MIN_TILES": "1", "HCRAG_PREPASS_TOPK": "1"},          # the top-k' pre-pass form
+    {"HCRAG_NO_PREPASS": "1"}])                  # cold per-workgroup bounds (no seed at all)
 def test_prepass_seed_parity(env):
     """The sampling pre-pass forced on small corpora: ids identical to the oracle whatever the
     seed, certificates complete after widening."""
