@@ -403,7 +403,11 @@ struct V3Cfg { int rt, qt, nst; };
 static V3Cfg v3_cfg(int nq) {
   if (nq <= 16) return {256, 16, 8};
   if (nq <= 64) return {256, 64, 7};
-  if (nq <= 128) return {256, 128, 6};
+  // 65-128 queries: the 256 x 256 kernel (half its query columns padded, MAXONLY pre-pass,
+  // UNIT epilogue) beats 256 x 128 (r01g sweeps: 10M x 768 B = 200 4.51 ms vs B = 128 4.74 ms
+  // on 256 x 128; 1M x 384 0.31 vs 0.57 ms).  HCRAG_QT128=1 keeps 256 x 128 for A/B.
+  static const bool qt128 = getenv("HCRAG_QT128") != nullptr;
+  if (nq <= 128 && qt128) return {256, 128, 6};
   // large batches: v4 (256 x 256, NST 4) unless HCRAG_V3_LARGE=1 keeps v3's 224 x 256
   static const bool v3_large = getenv("HCRAG_V3_LARGE") != nullptr;
   return v3_large ? V3Cfg{224, 256, 5} : V3Cfg{256, 256, 4};
@@ -646,6 +650,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // and skip the pre-pass -- a repeated identical batch then runs with the final bound
   static const bool keep_taug = getenv("HCRAG_DEBUG_KEEP_TAUG") != nullptr;
   if (!keep_taug) HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
+  // Padded query columns (q^ = 0, every score 0) get the bound ord32(+inf): with bound 0 they
+  // passed the epilogue's tile test on every tile and sent their waves down the exact path
+  // (r01g: B = 1 on the 256 x 16 tiles slower than B = 16).  Nothing reads their lists.
+  static const bool no_pad_bound = getenv("HCRAG_NO_PAD_BOUND") != nullptr;   // A/B switch
+  if (!keep_taug && !no_pad_bound && nqpad > nq)
+    HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ix->w_taug.as<uint32_t>() + nq),
+                           (int)0xFF800000u, (size_t)(nqpad - nq), st));
   HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
   HIPC(hipMemsetAsync(ix->w_tauest.p, 0, (size_t)nqpad * 4, st));   // 0 = no estimated bound
 
