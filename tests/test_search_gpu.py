@@ -310,9 +310,10 @@ def test_large_planted_recall_and_subset_parity(hc):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("B", [1, 130, 384, 700])
+@pytest.mark.parametrize("B", [1, 40, 100, 130, 384, 700])
 def test_batch_sizes_both_kernels(hc, dtype, B):
-    """B < 384 runs the 128x128 kernel, B >= 384 the 256x256 LDS-DMA kernel."""
+    """Every tile shape: 256 x 16 (B <= 16), 256 x 64 (17-64), 256 x 256 (> 64; padded query
+    columns at 100 and 130)."""
     rng = np.random.default_rng(B)
     N, D, k = 20000, 384, 10
     E = rng.standard_normal((N, D)).astype(np.float32)
