@@ -399,9 +399,19 @@ static int dispatch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, 
 }
 
 // ---- K2 v3 (score_v3.h): tile configurations by batch size ----
+static constexpr int64_t kQ64WideMaxElems = 2000000000;   // rows x ld, see v3_cfg
 struct V3Cfg { int rt, qt, nst; };
-static V3Cfg v3_cfg(int nq) {
+static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
   if (nq <= 16) return {256, 16, 8};
+  // 33-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
+  // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
+  // 1M x 768 0.49 vs 0.52, 2.5M x 768 1.11 vs 1.08, 5M x 768 2.13 vs 1.98, 10M x 768 4.13 vs
+  // 3.73 -> the crossover is near 2e9 corpus elements.  HCRAG_Q64_ELEMS overrides it.
+  static const int64_t q64_elems = [] {
+    const char* e = getenv("HCRAG_Q64_ELEMS");
+    return e ? (int64_t)atoll(e) : kQ64WideMaxElems;
+  }();
+  if (nq > 32 && nq <= 64 && n_rows * (int64_t)ld <= q64_elems) return {256, 256, 4};
   if (nq <= 64) return {256, 64, 7};
   // 65-128 queries: the 256 x 256 kernel (half its query columns padded, MAXONLY pre-pass,
   // UNIT epilogue) beats 256 x 128 (r01g sweeps: 10M x 768 B = 200 4.51 ms vs B = 128 4.74 ms
@@ -617,7 +627,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   int ver = ix->dtype == HCR_F32 ? 1 : (forced ? forced : 3);
   if (ver == 2 && nq < kV2MinQueries) ver = 1;
   if (ix->dtype == HCR_F32) ver = 1;
-  const V3Cfg c3 = v3_cfg(nq);
+  const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld);
   if (ver == 3 && !v3_fits(ix, c3)) ver = 1;
   const bool v2 = ver == 2;
   const int tq = ver == 3 ? c3.qt : v2 ? Q2 : BQ, tr = ver == 3 ? c3.rt : v2 ? R2 : BR;

@@ -310,10 +310,11 @@ def test_large_planted_recall_and_subset_parity(hc):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("B", [1, 40, 100, 130, 384, 700])
+@pytest.mark.parametrize("B", [1, 20, 40, 100, 130, 384, 700])
 def test_batch_sizes_both_kernels(hc, dtype, B):
-    """Every tile shape: 256 x 16 (B <= 16), 256 x 64 (17-64), 256 x 256 (> 64; padded query
-    columns at 100 and 130)."""
+    """Every tile shape: 256 x 16 (B <= 16), 256 x 64 (17-32, and 33-64 on large corpora),
+    256 x 256 (33-64 on small corpora such as this one, and > 64; padded query columns at
+    20, 40, 100 and 130)."""
     rng = np.random.default_rng(B)
     N, D, k = 20000, 384, 10
     E = rng.standard_normal((N, D)).astype(np.float32)
