@@ -399,19 +399,20 @@ static int dispatch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, 
 }
 
 // ---- K2 v3 (score_v3.h): tile configurations by batch size ----
-static constexpr int64_t kQ64WideMaxElems = 2000000000;   // rows x ld, see v3_cfg
+static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_cfg
 struct V3Cfg { int rt, qt, nst; };
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
   if (nq <= 16) return {256, 16, 8};
-  // 33-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
+  // 17-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
   // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
   // 1M x 768 0.49 vs 0.52, 2.5M x 768 1.11 vs 1.08, 5M x 768 2.13 vs 1.98, 10M x 768 4.13 vs
-  // 3.73 -> the crossover is near 2e9 corpus elements.  HCRAG_Q64_ELEMS overrides it.
+  // 3.73 -> the crossover is between 0.8e9 and 1.9e9 corpus elements (the cost of either tile
+  // shape is flat in the batch within its range).  HCRAG_Q64_ELEMS overrides it.
   static const int64_t q64_elems = [] {
     const char* e = getenv("HCRAG_Q64_ELEMS");
     return e ? (int64_t)atoll(e) : kQ64WideMaxElems;
   }();
-  if (nq > 32 && nq <= 64 && n_rows * (int64_t)ld <= q64_elems) return {256, 256, 4};
+  if (nq <= 64 && n_rows * (int64_t)ld <= q64_elems) return {256, 256, 4};
   if (nq <= 64) return {256, 64, 7};
   // 65-128 queries: the 256 x 256 kernel (half its query columns padded, MAXONLY pre-pass,
   // UNIT epilogue) beats 256 x 128 (r01g sweeps: 10M x 768 B = 200 4.51 ms vs B = 128 4.74 ms

@@ -312,9 +312,9 @@ def test_large_planted_recall_and_subset_parity(hc):
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
 @pytest.mark.parametrize("B", [1, 20, 40, 100, 130, 384, 700])
 def test_batch_sizes_both_kernels(hc, dtype, B):
-    """Every tile shape: 256 x 16 (B <= 16), 256 x 64 (17-32, and 33-64 on large corpora),
-    256 x 256 (33-64 on small corpora such as this one, and > 64; padded query columns at
-    20, 40, 100 and 130)."""
+    """Tile shapes 256 x 16 (B <= 16) and 256 x 256 (17-64 queries on small corpora such as
+    this one, and > 64; padded query columns at 20, 40, 100 and 130).  256 x 64 (17-64 queries
+    on large corpora): test_narrow_tiles_forced."""
     rng = np.random.default_rng(B)
     N, D, k = 20000, 384, 10
     E = rng.standard_normal((N, D)).astype(np.float32)
@@ -327,6 +327,43 @@ def test_batch_sizes_both_kernels(hc, dtype, B):
         es, ei = O.cosine_topk(Q, R, k)
         _check(s, i, es, ei)
         assert ix.last_stats()["uncertified_queries"] == 0
+
+
+_NARROW = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import hcrag_amd as hc
+from oracle import cosine_topk as O
+for B in (20, 40, 64):
+    rng = np.random.default_rng(B)
+    N, D, k = 30000, 384, 10
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[: B // 2] = E[rng.integers(0, N, B // 2)] + 0.2 * rng.standard_normal((B // 2, D)).astype(np.float32)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, R, k)
+        assert np.array_equal(i, ei), B
+        assert np.max(np.abs(s - es)) < 1e-6, B
+        assert ix.last_stats()["uncertified_queries"] == 0
+print("narrow ok")
+"""
+
+
+@pytest.mark.parametrize("min_tiles", ["1", "32"])
+def test_narrow_tiles_forced(min_tiles):
+    """The 256 x 64 tiles (17-64 queries on corpora above HCRAG_Q64_ELEMS) forced on a small
+    corpus, with and without the pre-pass, in a subprocess (the switches are read once)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HCRAG_Q64_ELEMS="0", HCRAG_PREPASS_MIN_TILES=min_tiles)
+    r = subprocess.run([sys.executable, "-c", _NARROW, root, os.path.join(root, "hc-rag_amd")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "narrow ok" in r.stdout
 
 
 def test_large_batch_mask_and_widening(hc):
