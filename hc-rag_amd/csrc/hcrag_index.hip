@@ -536,7 +536,7 @@ static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t 
 template <typename TS>
 static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d_q, int nq, int kp, int k, int mode,
                            double thr, double* out_s, int64_t* out_i, hipStream_t st) {
-  const size_t lds = (size_t)ix->dim * 8 + (size_t)kp * 24 + 16;
+  const size_t lds = (size_t)ix->dim * 8 + (size_t)kp * 32 + 16;
   hipLaunchKernelGGL((rescore_kernel<TS>), dim3(nq), dim3(256), lds, st, merged,
                      kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
                      ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,

@@ -742,30 +742,55 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
   uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
   uint64_t* lo = hi + kp;
   uint64_t* keys = lo + kp;
-  int& s_nvalid = *reinterpret_cast<int*>(keys + kp);   // all LDS in the dynamic region
+  double* nrm = reinterpret_cast<double*>(keys + kp);   // candidate row norms
+  int& s_nvalid = *reinterpret_cast<int*>(nrm + kp);    // all LDS in the dynamic region
   const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* src = q32 + (int64_t)q * dim;
   for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];
-  for (int c = threadIdx.x; c < kp; c += blockDim.x) keys[c] = merged[(size_t)q * kp + c];
+  for (int c = threadIdx.x; c < kp; c += blockDim.x) {   // row norms gathered up front
+    const uint64_t key = merged[(size_t)q * kp + c];
+    keys[c] = key;
+    nrm[c] = key ? norm64[key_row(key)] : 1.0;
+  }
   if (threadIdx.x == 0) s_nvalid = 0;
   __syncthreads();
   const double qn = qnorm[q];
-  for (int c = wave; c < kp; c += 4) {
-    const uint64_t key = keys[c];
-    if (key == 0ull) {
-      if (lane == 0) { hi[c] = 0ull; lo[c] = 0ull; }
-      continue;
+  // RU candidates per wave at a time, their row gathers in flight together; per candidate
+  // the summation order is the same as one at a time (lane-strided, then the wave sum)
+  constexpr int RU = 8;
+  for (int c0 = wave * RU; c0 < kp; c0 += 4 * RU) {
+    uint64_t kk[RU];
+    const TS* e[RU];
+    double acc[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      kk[u] = c0 + u < kp ? keys[c0 + u] : 0ull;
+      e[u] = rows + (int64_t)(kk[u] ? key_row(kk[u]) : 0u) * ld;
+      acc[u] = 0.0;
     }
-    const uint32_t row = key_row(key);
-    const TS* e = rows + (int64_t)row * ld;
-    double acc = 0.0;
-    for (int d = lane; d < dim; d += 64) acc += qd[d] * (double)(float)e[d];
-    acc = wave_sum_f64(acc);
-    if (lane == 0) {
-      const double s = acc / (qn * norm64[row]);
-      hi[c] = ord64(s);
-      lo[c] = (uint64_t)(0xFFFFFFFFu - row);
-      atomicAdd(&s_nvalid, 1);
+    for (int d = lane; d < dim; d += 64) {
+      const double qv = qd[d];
+      float x[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) x[u] = kk[u] ? (float)e[u][d] : 0.f;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) acc[u] += qv * (double)x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int c = c0 + u;
+      if (c >= kp) break;
+      const double a = wave_sum_f64(acc[u]);
+      if (lane == 0) {
+        if (kk[u] == 0ull) {
+          hi[c] = 0ull; lo[c] = 0ull;
+        } else {
+          const uint32_t row = key_row(kk[u]);
+          hi[c] = ord64(a / (qn * nrm[c]));
+          lo[c] = (uint64_t)(0xFFFFFFFFu - row);
+          atomicAdd(&s_nvalid, 1);
+        }
+      }
     }
   }
   __syncthreads();
