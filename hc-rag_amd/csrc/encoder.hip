@@ -6,6 +6,14 @@
 // BertModel forward (transformers modeling_bert: embeddings -> N x [self-attention ->
 // dense+residual+LayerNorm -> dense+GELU -> dense+residual+LayerNorm]) followed by the
 // sentence-transformers Pooling (mean over the attention mask, or CLS) and Normalize.
+//
+// Compute modes (hcr_encoder_create's compute_dtype):
+//   HCR_F16 / HCR_BF16  fast: MFMA operands in f16 / bf16, fp32 accumulation, LayerNorm,
+//                       softmax and residual stream;
+//   HCR_F32             reference precision (the reference encodes in fp32 torch,
+//                       experiments/embedding_generator.py:124): every projection GEMM as the
+//                       three-term split-f16 product on the same MFMA kernel (~22-bit operands,
+//                       fp32 accumulation), fp32 attention, library erff / expf.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -16,7 +24,6 @@
 
 #include "encoder_kernels.h"
 #include "gemm_v4.h"
-#include "gemm_p.h"
 #include "hcrag.h"
 #include "host_common.h"
 
@@ -24,24 +31,39 @@ using namespace hcr;
 
 struct EncLayer {
   DevBuf wqkv, bqkv, wo, bo, ln1g, ln1b, wi, bi, wo2, bo2, ln2g, ln2b;
+  // GEMM output scales (reference-precision mode: undo the weights' power-of-two scale and
+  // the split's 2^11; 1 in the fast modes)
+  float sqkv = 1.f, so = 1.f, si = 1.f, so2 = 1.f;
 };
 
 struct hcr_encoder {
   int device = 0;
   hcr_bert_config cfg{};
-  int dtype = HCR_F16;           // MFMA operand dtype (activations + projection weights)
+  int dtype = HCR_F16;           // HCR_F16 / HCR_BF16 (fast) or HCR_F32 (split-f16 reference precision)
   hipStream_t stream = nullptr;
   std::map<std::string, std::vector<float>> host;   // weights until finalize
   bool ready = false;
   DevBuf wemb, pemb, temb, embg, embb;
   std::vector<EncLayer> layers;
   // workspace
-  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out, trash;
-  int num_cus = 256;
+  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out;
   size_t att_lds_limit = 64 * 1024;
 };
 
 static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
+// forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover).
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false; };
+static const EncHooks& enc_hooks() {
+  static const EncHooks h = [] {
+    EncHooks t;
+    if (const char* e = getenv("HCRAG_GEMM_FT")) t.gemm_ft = atoi(e);
+    t.ln_scalar = getenv("HCRAG_LN_SCALAR") != nullptr;
+    return t;
+  }();
+  return h;
+}
 
 extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int compute_dtype,
                                   hcr_encoder** out) {
@@ -55,8 +77,8 @@ extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int co
   if (c.layers <= 0 || c.vocab_size <= 0 || c.max_position <= 0 || c.type_vocab <= 0)
     return hcr_set_error(HCR_EINVAL, "bad config sizes");
   if (c.pooling != 0 && c.pooling != 1) return hcr_set_error(HCR_EINVAL, "pooling must be 0 (mean) or 1 (cls)");
-  if (compute_dtype != HCR_F16 && compute_dtype != HCR_BF16)
-    return hcr_set_error(HCR_EINVAL, "compute dtype must be HCR_F16 or HCR_BF16");
+  if (compute_dtype != HCR_F16 && compute_dtype != HCR_BF16 && compute_dtype != HCR_F32)
+    return hcr_set_error(HCR_EINVAL, "compute dtype must be HCR_F16, HCR_BF16 or HCR_F32");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
   if (device < 0 || device >= ndev)
@@ -66,9 +88,6 @@ extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int co
   e->device = device;
   e->cfg = c;
   e->dtype = compute_dtype;
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
-    e->num_cus = cus;
   hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (he != hipSuccess) {
     delete e;
@@ -83,7 +102,7 @@ extern "C" int hcr_encoder_destroy(hcr_encoder* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   DevBuf* bufs[] = {&e->wemb, &e->pemb, &e->temb, &e->embg, &e->embb, &e->ids, &e->mask, &e->x,
-                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out, &e->trash};
+                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out};
   for (DevBuf* b : bufs) b->release();
   for (auto& L : e->layers) {
     DevBuf* lb[] = {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.ln1g, &L.ln1b, &L.wi, &L.bi, &L.wo2, &L.bo2, &L.ln2g, &L.ln2b};
@@ -93,6 +112,8 @@ extern "C" int hcr_encoder_destroy(hcr_encoder* e) {
   delete e;
   return HCR_OK;
 }
+
+extern "C" int hcr_encoder_compute_dtype(const hcr_encoder* e) { return e ? e->dtype : -1; }
 
 // HF BertModel state-dict name, any prefix before "embeddings." / "encoder." is ignored
 // (sentence-transformers checkpoints use "0.auto_model." or none; BertForX uses "bert.").
@@ -110,16 +131,33 @@ extern "C" int hcr_encoder_set_weight(hcr_encoder* e, const char* name, const fl
   return HCR_OK;
 }
 
-template <typename TM>
-static int upload_padded(DevBuf& dst, const std::vector<float>& src, int64_t rows, int64_t cols,
-                         int64_t rows_pad, hipStream_t st) {
-  CHECK(dst.ensure((size_t)rows_pad * cols * sizeof(TM)));
+// Projection weights [rows][cols] fp32 -> device, rows padded with zeros to rows_pad.
+// Fast modes: MFMA dtype [rows_pad][cols].  Reference-precision mode: split f16
+// [rows_pad][3 cols] scaled by a power of two (max |W| -> ~16); *oscale receives the factor
+// that the GEMM epilogue applies.
+template <typename TM, bool SPLIT>
+static int upload_weights(DevBuf& dst, const std::vector<float>& src, int64_t rows, int64_t cols,
+                          int64_t rows_pad, float* oscale, hipStream_t st) {
+  const int w = SPLIT ? 3 : 1;
+  CHECK(dst.ensure((size_t)rows_pad * cols * w * sizeof(TM)));
   DevBuf tmp;
   CHECK(tmp.ensure((size_t)rows * cols * 4));
   HIPC(hipMemcpyAsync(tmp.p, src.data(), (size_t)rows * cols * 4, hipMemcpyHostToDevice, st));
   const int64_t tot = rows_pad * cols;
-  hipLaunchKernelGGL((to_mfma_dtype<TM>), dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
-                     tmp.as<const float>(), rows, rows_pad, (int)cols, dst.as<TM>());
+  const dim3 grid((unsigned)((tot + 255) / 256));
+  if constexpr (SPLIT) {
+    float mx = 0.f;
+    for (size_t i = 0; i < (size_t)(rows * cols); ++i) mx = std::max(mx, std::fabs(src[i]));
+    const int e2 = mx > 0.f ? (int)std::floor(std::log2(16.0 / mx)) : 0;
+    const float scale = std::ldexp(1.f, e2);
+    hipLaunchKernelGGL(to_split_weights, grid, dim3(256), 0, st, tmp.as<const float>(), rows,
+                       rows_pad, (int)cols, scale, dst.as<_Float16>());
+    *oscale = 1.f / (scale * kSplitLo);
+  } else {
+    hipLaunchKernelGGL((to_mfma_dtype<TM>), grid, dim3(256), 0, st, tmp.as<const float>(), rows,
+                       rows_pad, (int)cols, dst.as<TM>());
+    *oscale = 1.f;
+  }
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(st));
   tmp.release();
@@ -133,7 +171,7 @@ static int upload_f32(DevBuf& dst, const float* src, size_t n, size_t n_pad, hip
   return HCR_OK;
 }
 
-template <typename TM>
+template <typename TM, bool SPLIT>
 static int finalize_t(hcr_encoder* e) {
   const auto& c = e->cfg;
   const int H = c.hidden, F = c.intermediate;
@@ -187,15 +225,15 @@ static int finalize_t(hcr_encoder* e) {
     std::memcpy(bqkv.data(), bq->data(), H * 4);
     std::memcpy(bqkv.data() + H, bk->data(), H * 4);
     std::memcpy(bqkv.data() + 2 * H, bv->data(), H * 4);
-    CHECK(upload_padded<TM>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 768), st));
+    CHECK((upload_weights<TM, SPLIT>(L.wqkv, wqkv, 3 * H, H, rup(3 * H, 768), &L.sqkv, st)));
     CHECK(upload_f32(L.bqkv, bqkv.data(), 3 * H, rup(3 * H, 768), st));
-    CHECK(upload_padded<TM>(L.wo, *wo, H, H, rup(H, 768), st));
+    CHECK((upload_weights<TM, SPLIT>(L.wo, *wo, H, H, rup(H, 768), &L.so, st)));
     CHECK(upload_f32(L.bo, bo->data(), H, rup(H, 768), st));
     CHECK(upload_f32(L.ln1g, g1->data(), H, H, st));
     CHECK(upload_f32(L.ln1b, b1->data(), H, H, st));
-    CHECK(upload_padded<TM>(L.wi, *wi, F, H, rup(F, 768), st));
+    CHECK((upload_weights<TM, SPLIT>(L.wi, *wi, F, H, rup(F, 768), &L.si, st)));
     CHECK(upload_f32(L.bi, bi->data(), F, rup(F, 768), st));
-    CHECK(upload_padded<TM>(L.wo2, *wo2, H, F, rup(H, 768), st));
+    CHECK((upload_weights<TM, SPLIT>(L.wo2, *wo2, H, F, rup(H, 768), &L.so2, st)));
     CHECK(upload_f32(L.bo2, bo2->data(), H, rup(H, 768), st));
     CHECK(upload_f32(L.ln2g, g2->data(), H, H, st));
     CHECK(upload_f32(L.ln2b, b2->data(), H, H, st));
@@ -207,65 +245,43 @@ static int finalize_t(hcr_encoder* e) {
 extern "C" int hcr_encoder_finalize(hcr_encoder* e) {
   if (!e) return hcr_set_error(HCR_EINVAL, "encoder is NULL");
   HIPC(hipSetDevice(e->device));
-  int rc = e->dtype == HCR_F16 ? finalize_t<_Float16>(e) : finalize_t<__bf16>(e);
+  int rc = e->dtype == HCR_F16    ? finalize_t<_Float16, false>(e)
+           : e->dtype == HCR_BF16 ? finalize_t<__bf16, false>(e)
+                                  : finalize_t<_Float16, true>(e);
   if (rc != HCR_OK) return rc;
   e->host.clear();
   e->ready = true;
   return HCR_OK;
 }
 
+// C = oscale * X . W^T + bias (+ epilogue) on the LDS-DMA ring GEMM (gemm_v4.h).  K is the
+// operand row length (3 x the model width in the reference-precision mode).
 template <typename TM, int EPI>
 static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const float* bias,
-                       const float* resid, TM* out_h, float* out_f, int ldo, hipStream_t st) {
-  // gfx950 path: LDS-DMA ring GEMM (gemm_v4.h); HCRAG_GEMM_V1=1 keeps the register-staged
-  // 128 x 128 kernel for A/B checks
-  static const bool v1 = getenv("HCRAG_GEMM_V1") != nullptr;
-  if (!v1 && K % V3_BK == 0) {
-    // feature tile: 192 when it fills the last round of 256-CU workgroups better than 256
-    // (N = 768 at T = 32768: 512 tiles = 2 full rounds vs 384 = 1.5); weights are padded to
-    // a multiple of 768 rows so either tile reads whole rows.  HCRAG_GEMM_FT=256|192 forces.
-    static const int force_ft = [] {
-      const char* e = getenv("HCRAG_GEMM_FT");
-      return e ? atoi(e) : 0;
-    }();
-    const int ntt = (int)(rup(T, G4_T) / G4_T);
-    auto rounds = [&](int ft) {            // rounds of 256 resident workgroups
-      const int64_t tiles = rup(N, ft) / ft * (int64_t)ntt;
-      return (double)((tiles + 255) / 256);
-    };
-    // a 192-feature tile takes ~0.94x the time of a 256-feature one (r01c: QKV 183 vs 163 us
-    // at 6 vs 5 rounds), not 0.75x: it pays only where it removes a mostly-empty round
-    const bool ft192 = force_ft ? force_ft == 192 : (rounds(192) * 0.94 < rounds(256));
-    if (ft192) {
-      const int nft = (int)(rup(N, 192) / 192);
-      hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 192>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
-                         0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
-    } else {
-      const int nft = (int)(rup(N, G4_T) / G4_T);
-      hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 256>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
-                         0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo);
-    }
-    HIPC(hipGetLastError());
-    return HCR_OK;
+                       const float* resid, TM* out_h, float* out_f, int ldo, float oscale,
+                       hipStream_t st) {
+  if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
+  // feature tile: 192 when it fills the last round of 256-CU workgroups better than 256
+  // (N = 768 at T = 32768: 512 tiles = 2 full rounds vs 384 = 1.5); weights are padded to
+  // a multiple of 768 rows so either tile reads whole rows.
+  const int ntt = (int)(rup(T, G4_T) / G4_T);
+  auto rounds = [&](int ft) {            // rounds of 256 resident workgroups
+    const int64_t tiles = rup(N, ft) / ft * (int64_t)ntt;
+    return (double)((tiles + 255) / 256);
+  };
+  // a 192-feature tile takes ~0.94x the time of a 256-feature one (r01c: QKV 183 vs 163 us
+  // at 6 vs 5 rounds), not 0.75x: it pays only where it removes a mostly-empty round
+  const int force_ft = enc_hooks().gemm_ft;
+  const bool ft192 = force_ft ? force_ft == 192 : (rounds(192) * 0.94 < rounds(256));
+  if (ft192) {
+    const int nft = (int)(rup(N, 192) / 192);
+    hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 192>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
+                       0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  } else {
+    const int nft = (int)(rup(N, G4_T) / G4_T);
+    hipLaunchKernelGGL((gemm_v4_kernel<TM, EPI, 4, 256>), dim3((unsigned)(nft * ntt)), dim3(V3_NT),
+                       0, st, W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
   }
-  const int nft = (int)(rup(N, BR) / BR), ntt = (int)(rup(T, BQ) / BQ);
-  hipLaunchKernelGGL((gemm_nt_kernel<TM, EPI>), dim3((unsigned)(nft * ntt)), dim3(256), 0, st, W, X,
-                     K, N, T, nft, bias, resid, out_h, out_f, ldo);
-  HIPC(hipGetLastError());
-  return HCR_OK;
-}
-
-// Persistent ring GEMM (gemm_p.h): min(tiles, CUs) workgroups, each streaming a contiguous
-// share of the 256 x 256 tiles (feature tile fastest, so consecutive tiles share X).
-// EPI_BIAS_RESID writes projection + bias only (the residual is added by the LayerNorm).
-template <typename TM, int EPI>
-static int launch_gemm_p(hcr_encoder* e, const TM* W, const TM* X, int K, int N, int T,
-                         const float* bias, TM* out_h, float* out_f, int ldo, hipStream_t st) {
-  const int nft = (int)(rup(N, GP_T) / GP_T), ntt = (int)(rup(T, GP_T) / GP_T);
-  const int tiles = nft * ntt;
-  const int grid = std::min(tiles, e->num_cus);
-  hipLaunchKernelGGL((gemm_p_kernel<TM, EPI, 4>), dim3((unsigned)grid), dim3(V3_NT), 0, st, W, X,
-                     K, N, T, nft, tiles, bias, out_h, out_f, ldo, e->trash.as<float4>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -274,12 +290,9 @@ template <typename TM, int DH, int KB>
 static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
                                  hipStream_t st) {
   const size_t lds = attention_mfma_lds<TM, DH>(S);
-  static bool attr_set = false;          // one process-wide attribute per instantiation
-  if (lds > 64 * 1024 && !attr_set) {
+  if (lds > 64 * 1024)
     HIPC(hipFuncSetAttribute((const void*)attention_mfma_kernel<TM, DH, KB>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
   hipLaunchKernelGGL((attention_mfma_kernel<TM, DH, KB>), dim3((unsigned)(n * e->cfg.heads)),
                      dim3(256), lds, st, e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden,
                      e->cfg.heads, e->ctx.as<TM>());
@@ -287,119 +300,115 @@ static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t 
   return HCR_OK;
 }
 
-// MFMA attention for head dims 32 / 64 up to 512 keys; the scalar kernel otherwise
-// (HCRAG_SCALAR_ATTENTION=1 forces it, for A/B checks).
+// Fast modes: MFMA attention for head dims 32 / 64 up to 512 keys, the scalar kernel otherwise.
 template <typename TM>
 static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
-                            hipStream_t st, size_t scalar_lds) {
-  static const bool force_scalar = getenv("HCRAG_SCALAR_ATTENTION") != nullptr;
+                            hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
   const int Sp = (S + 31) & ~31;
-  if (!force_scalar && (dh == 32 || dh == 64) && Sp <= 512) {
+  if ((dh == 32 || dh == 64) && Sp <= 512) {
     if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, d_mask, n, S, st)
                                    : launch_attention_mfma<TM, 32, 32>(e, d_mask, n, S, st);
     return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, d_mask, n, S, st)
                      : launch_attention_mfma<TM, 64, 32>(e, d_mask, n, S, st);
   }
-  hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * e->cfg.heads)), dim3(256),
-                     scalar_lds, st, e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden,
-                     e->cfg.heads, e->ctx.as<TM>());
+  const size_t lds = (size_t)(5 * S + 4 * dh) * 4 + (size_t)2 * S * dh * sizeof(TM);
+  if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
+  if (lds > 64 * 1024)
+    HIPC(hipFuncSetAttribute((const void*)attention_kernel<TM>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
+                     e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<TM>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
-template <typename TM>
+// Reference-precision mode: fp32 attention, K/V in LDS when the sequence fits.
+static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+                                hipStream_t st) {
+  const int dh = e->cfg.hidden / e->cfg.heads;
+  const bool kv_lds = attention_f32_lds(S, dh, true) <= 160 * 1024;
+  const size_t lds = attention_f32_lds(S, dh, kv_lds);
+  if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
+  const void* fn = kv_lds ? (const void*)attention_f32_kernel<true> : (const void*)attention_f32_kernel<false>;
+  if (lds > 64 * 1024) HIPC(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  if (kv_lds)
+    hipLaunchKernelGGL((attention_f32_kernel<true>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
+                       e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+  else
+    hipLaunchKernelGGL((attention_f32_kernel<false>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
+                       e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+template <typename TM, bool SPLIT>
 static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask, int64_t n, int S,
                     float* d_out, hipStream_t st) {
   const auto& c = e->cfg;
-  const int H = c.hidden, F = c.intermediate, NH = c.heads, dh = H / NH;
+  const int H = c.hidden, F = c.intermediate;
+  const int w = SPLIT ? 3 : 1;                        // activation row width factor
   const int64_t T = n * (int64_t)S, Tp = rup(T, 256);
   if (T > (int64_t)1 << 30) return hcr_set_error(HCR_EINVAL, "batch too large");
   CHECK(e->x.ensure((size_t)Tp * H * 4));
   CHECK(e->y.ensure((size_t)Tp * H * 4));
-  CHECK(e->xh.ensure((size_t)Tp * H * sizeof(TM)));
-  CHECK(e->ctx.ensure((size_t)Tp * H * sizeof(TM)));
-  CHECK(e->qkv.ensure((size_t)Tp * 3 * H * sizeof(TM)));
-  CHECK(e->inter.ensure((size_t)Tp * F * sizeof(TM)));
+  CHECK(e->xh.ensure((size_t)Tp * H * w * sizeof(TM)));
+  CHECK(e->ctx.ensure((size_t)Tp * H * w * sizeof(TM)));
+  CHECK(e->qkv.ensure((size_t)Tp * 3 * H * (SPLIT ? 4 : sizeof(TM))));
+  CHECK(e->inter.ensure((size_t)Tp * F * w * sizeof(TM)));
   const unsigned gT = (unsigned)((T + 3) / 4);
   // vectorised LayerNorm kernels when H % 4 == 0 and H <= 1024 (all BERT widths here)
-  const bool ln4 = (H % 4 == 0) && H <= 1024 && !getenv("HCRAG_LN_SCALAR");
+  const bool ln4 = (H % 4 == 0) && H <= 1024 && !enc_hooks().ln_scalar;
   auto layer_norm = [&](const DevBuf& g, const DevBuf& bb) {
     if (ln4)
-      hipLaunchKernelGGL((layernorm4_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+      hipLaunchKernelGGL((layernorm4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
                          e->x.as<float>(), e->xh.as<TM>());
     else
-      hipLaunchKernelGGL((layernorm_kernel<TM>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+      hipLaunchKernelGGL((layernorm_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
                          e->x.as<float>(), e->xh.as<TM>());
   };
   if (ln4)
-    hipLaunchKernelGGL((embed_ln4_kernel<TM>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+    hipLaunchKernelGGL((embed_ln4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
                        e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
   else
-  hipLaunchKernelGGL((embed_ln_kernel<TM>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
-                     e->wemb.as<const float>(), e->pemb.as<const float>(),
-                     e->temb.as<const float>(), e->embg.as<const float>(),
-                     e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+    hipLaunchKernelGGL((embed_ln_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+                       e->wemb.as<const float>(), e->pemb.as<const float>(),
+                       e->temb.as<const float>(), e->embg.as<const float>(),
+                       e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
   HIPC(hipGetLastError());
-  const size_t att_lds = (size_t)(5 * S + 4 * dh) * 4 + (size_t)2 * S * dh * sizeof(TM);
-  if (att_lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
-  if (att_lds > e->att_lds_limit) {
-    HIPC(hipFuncSetAttribute((const void*)attention_kernel<TM>,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    e->att_lds_limit = 160 * 1024;
-  }
-  // persistent GEMMs + residual-adding LayerNorm: opt-in HCRAG_GEMM_P=1 (r01c: 95.7k vs
-  // 101.8k embeddings/s for the one-tile-per-workgroup GEMMs, profiles/r01c); needs K >= 64
-  static const bool use_p = getenv("HCRAG_GEMM_P") != nullptr;
-  if (use_p && ln4 && H % 32 == 0 && F % 32 == 0 && H >= 64) {
-    CHECK(e->trash.ensure(64 * 16));
-    auto ln_res = [&](const DevBuf& g, const DevBuf& bb) {
-      hipLaunchKernelGGL((layernorm4_res_kernel<TM>), dim3(gT), dim3(256), 0, st,
-                         e->y.as<const float>(), (int)T, H, g.as<const float>(),
-                         bb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
-    };
-    for (int l = 0; l < c.layers; ++l) {
-      const EncLayer& L = e->layers[l];
-      CHECK((launch_gemm_p<TM, EPI_BIAS>(e, L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H,
-                                         (int)T, L.bqkv.as<const float>(), e->qkv.as<TM>(), nullptr,
-                                         3 * H, st)));
-      CHECK(launch_attention<TM>(e, d_mask, n, S, st, att_lds));
-      CHECK((launch_gemm_p<TM, EPI_BIAS_RESID>(e, L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H,
-                                               (int)T, L.bo.as<const float>(), nullptr,
-                                               e->y.as<float>(), H, st)));
-      ln_res(L.ln1g, L.ln1b);
-      HIPC(hipGetLastError());
-      CHECK((launch_gemm_p<TM, EPI_BIAS_GELU>(e, L.wi.as<const TM>(), e->xh.as<const TM>(), H, F,
-                                              (int)T, L.bi.as<const float>(), e->inter.as<TM>(),
-                                              nullptr, F, st)));
-      CHECK((launch_gemm_p<TM, EPI_BIAS_RESID>(e, L.wo2.as<const TM>(), e->inter.as<const TM>(), F,
-                                               H, (int)T, L.bo2.as<const float>(), nullptr,
-                                               e->y.as<float>(), H, st)));
-      ln_res(L.ln2g, L.ln2b);
-      HIPC(hipGetLastError());
-    }
-  } else
   for (int l = 0; l < c.layers; ++l) {
     const EncLayer& L = e->layers[l];
-    CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
-                                     L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
-                                     3 * H, st)));
-    CHECK(launch_attention<TM>(e, d_mask, n, S, st, att_lds));
-    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H, (int)T,
-                                           L.bo.as<const float>(), e->x.as<const float>(), nullptr,
-                                           e->y.as<float>(), H, st)));
+    if constexpr (SPLIT) {
+      CHECK((launch_gemm<TM, EPI_BIAS_F32>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), 3 * H, 3 * H,
+                                           (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
+                                           e->qkv.as<float>(), 3 * H, L.sqkv, st)));
+      CHECK(launch_attention_f32(e, d_mask, n, S, st));
+    } else {
+      CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
+                                       L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
+                                       3 * H, L.sqkv, st)));
+      CHECK(launch_attention<TM>(e, d_mask, n, S, st));
+    }
+    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H * w, H,
+                                           (int)T, L.bo.as<const float>(), e->x.as<const float>(),
+                                           nullptr, e->y.as<float>(), H, L.so, st)));
     layer_norm(L.ln1g, L.ln1b);
     HIPC(hipGetLastError());
-    CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
-                                          L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
-                                          nullptr, F, st)));
-    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F, H,
+    if constexpr (SPLIT)
+      CHECK((launch_gemm<TM, EPI_BIAS_GELU_SPLIT>(L.wi.as<const TM>(), e->xh.as<const TM>(), 3 * H, F,
+                                                  (int)T, L.bi.as<const float>(), nullptr,
+                                                  e->inter.as<TM>(), nullptr, F, L.si, st)));
+    else
+      CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
+                                            L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
+                                            nullptr, F, L.si, st)));
+    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F * w, H,
                                            (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
-                                           nullptr, e->y.as<float>(), H, st)));
+                                           nullptr, e->y.as<float>(), H, L.so2, st)));
     layer_norm(L.ln2g, L.ln2b);
     HIPC(hipGetLastError());
   }
@@ -419,8 +428,9 @@ extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int
   if (!d_ids || !d_mask || !d_out) return hcr_set_error(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;   // the caller's stream (NULL = legacy default)
-  return e->dtype == HCR_F16 ? encode_t<_Float16>(e, d_ids, d_mask, n, S, d_out, st)
-                             : encode_t<__bf16>(e, d_ids, d_mask, n, S, d_out, st);
+  if (e->dtype == HCR_F16) return encode_t<_Float16, false>(e, d_ids, d_mask, n, S, d_out, st);
+  if (e->dtype == HCR_BF16) return encode_t<__bf16, false>(e, d_ids, d_mask, n, S, d_out, st);
+  return encode_t<_Float16, true>(e, d_ids, d_mask, n, S, d_out, st);
 }
 
 extern "C" int hcr_encode(hcr_encoder* e, const int32_t* ids, const int32_t* mask, int64_t n, int S,

@@ -18,11 +18,47 @@
 namespace hcr {
 
 // -------------------------------------------------------------------------------------
+// Activation stores.  Fast modes (TM = f16 / bf16): the MFMA-dtype copy xh [T][n].
+// Reference-precision mode (SPLIT, TM = f16): a 3n-wide row [h | h | l] with h = f16(v) and
+// l = f16((v - h) * 2^11), the A operand of the three-term split GEMM (gemm_v4.h): against
+// weights stored [Wh * 2^11 | Wl * 2^11 | Wh] the K-concatenated product is
+// 2^11 (Xh Wh + Xh Wl + Xl Wh) in one fp32 accumulator -- about 22 bits of operand precision,
+// and the 2^11 keeps the low parts out of the f16 subnormal range.
+// -------------------------------------------------------------------------------------
+constexpr float kSplitLo = 2048.f;          // 2^11: f16 has an 11-bit significand
+
+template <typename TM, bool SPLIT>
+__device__ __forceinline__ void store_act4(TM* __restrict__ row, int n, int f, float4 o) {
+  union { TM h[4]; uint2 u; } ph;
+  ph.h[0] = (TM)o.x; ph.h[1] = (TM)o.y; ph.h[2] = (TM)o.z; ph.h[3] = (TM)o.w;
+  *reinterpret_cast<uint2*>(row + f) = ph.u;
+  if constexpr (SPLIT) {
+    union { TM h[4]; uint2 u; } pl;
+    pl.h[0] = (TM)((o.x - (float)ph.h[0]) * kSplitLo);
+    pl.h[1] = (TM)((o.y - (float)ph.h[1]) * kSplitLo);
+    pl.h[2] = (TM)((o.z - (float)ph.h[2]) * kSplitLo);
+    pl.h[3] = (TM)((o.w - (float)ph.h[3]) * kSplitLo);
+    *reinterpret_cast<uint2*>(row + n + f) = ph.u;
+    *reinterpret_cast<uint2*>(row + 2 * n + f) = pl.u;
+  }
+}
+template <typename TM, bool SPLIT>
+__device__ __forceinline__ void store_act1(TM* __restrict__ row, int n, int f, float v) {
+  const TM h = (TM)v;
+  row[f] = h;
+  if constexpr (SPLIT) {
+    row[n + f] = h;
+    row[2 * n + f] = (TM)((v - (float)h) * kSplitLo);
+  }
+}
+template <bool SPLIT> __host__ __device__ constexpr int act_width() { return SPLIT ? 3 : 1; }
+
+// -------------------------------------------------------------------------------------
 // Embedding gather + LayerNorm (one wave per token).  HF BertEmbeddings: word + position +
 // token_type(0), LayerNorm(eps), dropout (identity at inference).
 // -------------------------------------------------------------------------------------
 // row LayerNorm helper: values come from a functor (re-evaluated per pass; rows are L1-hot)
-template <typename TM, typename F>
+template <typename TM, bool SPLIT, typename F>
 __device__ __forceinline__ void ln_row(F val, int H, const float* __restrict__ g,
                                        const float* __restrict__ b, float eps, int lane,
                                        float* __restrict__ xo, TM* __restrict__ xho) {
@@ -37,7 +73,7 @@ __device__ __forceinline__ void ln_row(F val, int H, const float* __restrict__ g
   for (int d = lane; d < H; d += 64) {
     const float y = (val(d) - mean) * rstd * g[d] + b[d];
     xo[d] = y;
-    xho[d] = (TM)y;
+    store_act1<TM, SPLIT>(xho, H, d, y);
   }
 }
 
@@ -45,7 +81,7 @@ __device__ __forceinline__ void ln_row(F val, int H, const float* __restrict__ g
 // wave per row, the row held in registers as up to 4 float4 per lane (one HBM pass), float4
 // gamma/beta loads, 16-byte fp32 and 8-byte MFMA-dtype stores.  Same arithmetic as ln_row
 // (mean, then the centred second moment, rsqrtf(var + eps)).
-template <typename TM>
+template <typename TM, bool SPLIT>
 __device__ __forceinline__ void ln_row4(float4 (&v)[4], int H, const float* __restrict__ g,
                                         const float* __restrict__ b, float eps, int lane,
                                         float* __restrict__ xo, TM* __restrict__ xho) {
@@ -77,13 +113,11 @@ __device__ __forceinline__ void ln_row4(float4 (&v)[4], int H, const float* __re
     o.z = (v[i].z - mean) * rstd * gg.z + bb.z;
     o.w = (v[i].w - mean) * rstd * gg.w + bb.w;
     reinterpret_cast<float4*>(xo)[d4] = o;
-    union { TM h[4]; uint2 u; } pk;
-    pk.h[0] = (TM)o.x; pk.h[1] = (TM)o.y; pk.h[2] = (TM)o.z; pk.h[3] = (TM)o.w;
-    reinterpret_cast<uint2*>(xho)[d4] = pk.u;
+    store_act4<TM, SPLIT>(xho, H, 4 * d4, o);
   }
 }
 
-template <typename TM>
+template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
 layernorm4_kernel(const float* __restrict__ y, int T_real, int H, const float* __restrict__ g,
                   const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
@@ -95,36 +129,11 @@ layernorm4_kernel(const float* __restrict__ y, int T_real, int H, const float* _
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     v[i] = (lane + 64 * i < (H >> 2)) ? yr[lane + 64 * i] : float4{0.f, 0.f, 0.f, 0.f};
-  ln_row4<TM>(v, H, g, b, eps, lane, x + (size_t)t * H, xh + (size_t)t * H);
+  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x + (size_t)t * H,
+                     xh + (size_t)t * H * act_width<SPLIT>());
 }
 
-// LayerNorm of (projection + residual): v = y + x, then x <- LN(v) (in place: each wave holds
-// its row in registers before writing it) and xh <- MFMA-dtype copy.  The persistent GEMM
-// (gemm_p.h) writes the projection + bias only, so its epilogue has no global loads.
-template <typename TM>
-__global__ void __launch_bounds__(256)
-layernorm4_res_kernel(const float* __restrict__ y, int T_real, int H, const float* __restrict__ g,
-                      const float* __restrict__ b, float eps, float* x, TM* __restrict__ xh) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= T_real) return;
-  const float4* yr = reinterpret_cast<const float4*>(y + (size_t)t * H);
-  const float4* xr = reinterpret_cast<const float4*>(x + (size_t)t * H);
-  float4 v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int d4 = lane + 64 * i;
-    if (d4 < (H >> 2)) {
-      const float4 a = yr[d4], c = xr[d4];
-      v[i] = float4{a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w};
-    } else {
-      v[i] = float4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  ln_row4<TM>(v, H, g, b, eps, lane, x + (size_t)t * H, xh + (size_t)t * H);
-}
-
-template <typename TM>
+template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
 embed_ln4_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
                  const float* __restrict__ wemb, const float* __restrict__ pemb,
@@ -141,16 +150,18 @@ embed_ln4_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
   for (int i = 0; i < 4; ++i) {
     const int d4 = lane + 64 * i;
     if (d4 < (H >> 2)) {
+      // HF BertEmbeddings order: (word + token_type) + position
       const float4 a = w[d4], c = p[d4], e = ty[d4];
-      v[i] = float4{a.x + c.x + e.x, a.y + c.y + e.y, a.z + c.z + e.z, a.w + c.w + e.w};
+      v[i] = float4{(a.x + e.x) + c.x, (a.y + e.y) + c.y, (a.z + e.z) + c.z, (a.w + e.w) + c.w};
     } else {
       v[i] = float4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  ln_row4<TM>(v, H, g, b, eps, lane, x + (size_t)t * H, xh + (size_t)t * H);
+  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x + (size_t)t * H,
+                     xh + (size_t)t * H * act_width<SPLIT>());
 }
 
-template <typename TM>
+template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
 embed_ln_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
                 const float* __restrict__ wemb, const float* __restrict__ pemb,
@@ -161,12 +172,12 @@ embed_ln_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
   if (t >= T_real) return;
   const float* w = wemb + (size_t)ids[t] * H;
   const float* p = pemb + (size_t)(t % S) * H;
-  ln_row<TM>([&](int d) { return w[d] + p[d] + temb[d]; }, H, g, b, eps, lane,
-             x + (size_t)t * H, xh + (size_t)t * H);
+  ln_row<TM, SPLIT>([&](int d) { return (w[d] + temb[d]) + p[d]; }, H, g, b, eps, lane,
+                    x + (size_t)t * H, xh + (size_t)t * H * act_width<SPLIT>());
 }
 
 // LayerNorm of y (fp32, already = residual + sublayer output) -> x fp32 and xh MFMA dtype.
-template <typename TM>
+template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
 layernorm_kernel(const float* __restrict__ y, int T_real, int H, const float* __restrict__ g,
                  const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
@@ -174,22 +185,26 @@ layernorm_kernel(const float* __restrict__ y, int T_real, int H, const float* __
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T_real) return;
   const float* yr = y + (size_t)t * H;
-  ln_row<TM>([&](int d) { return yr[d]; }, H, g, b, eps, lane, x + (size_t)t * H,
-             xh + (size_t)t * H);
+  ln_row<TM, SPLIT>([&](int d) { return yr[d]; }, H, g, b, eps, lane, x + (size_t)t * H,
+                    xh + (size_t)t * H * act_width<SPLIT>());
 }
 
 // -------------------------------------------------------------------------------------
-// GEMM  C[token][feature] = sum_k xh[token][k] * W[feature][k] + bias[feature]  (+ epilogue)
-//   tile 128 features x 128 tokens, 4 waves (2 x 2), register-staged double-buffered LDS
-//   (same image / fragment reads as the score kernel v1).  M (features) and T (tokens) are
-//   padded to 128 by the caller; K % 64 == 0.
+// GEMM epilogues (gemm_v4.h):  C[token][feature] = oscale * sum_k X[token][k] W[feature][k]
+// + bias[feature], then
+//   EPI_BIAS            -> MFMA-dtype out_h [T][ldo]                   (fast QKV)
+//   EPI_BIAS_GELU       -> GELU, MFMA-dtype out_h [T][ldo]             (fast FFN1)
+//   EPI_BIAS_RESID      -> + resid fp32, fp32 out_f [T][ldo]           (O-proj / FFN2)
+//   EPI_BIAS_F32        -> fp32 out_f [T][ldo]                         (split QKV)
+//   EPI_BIAS_GELU_SPLIT -> exact-erf GELU, split out_h [T][3 ldo]      (split FFN1)
 // -------------------------------------------------------------------------------------
-enum : int { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESID = 2 };
+enum : int { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESID = 2, EPI_BIAS_F32 = 3,
+             EPI_BIAS_GELU_SPLIT = 4 };
 
 // GELU(x) = x/2 (1 + erf(x / sqrt 2)) (HF BERT "gelu", exact-erf form).  erf by Abramowitz &
 // Stegun 7.1.26 (|error| <= 1.5e-7, far below the fp16/bf16 output rounding) on v_rcp / v_exp:
 // ~12 instructions instead of the ~50 of the library erff -- the FFN1 epilogue evaluates 128 of
-// them per lane per tile.
+// them per lane per tile.  The reference-precision mode uses the library erff.
 __device__ __forceinline__ float erf_as(float x) {
   const float ax = fabsf(x);
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
@@ -202,96 +217,7 @@ __device__ __forceinline__ float erf_as(float x) {
   return copysignf(r, x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)); }
-
-template <typename TM, int EPI>
-__global__ void __launch_bounds__(256, 2)
-gemm_nt_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_real, int T_real,
-               int n_tiles_feat, const float* __restrict__ bias, const float* __restrict__ resid,
-               TM* __restrict__ out_h, float* __restrict__ out_f, int ldo) {
-  using Op = MfmaOp<TM>;
-  using V = typename Op::V;
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  // XCD-friendly order: consecutive blocks share the token tile (X re-read from L2)
-  const int ft = blockIdx.x % n_tiles_feat, tt = blockIdx.x / n_tiles_feat;
-  const int f0 = ft * BR, t0 = tt * BQ;
-  const TM* Wt = W + (size_t)f0 * K;
-  const TM* Xt = X + (size_t)t0 * K;
-  TileLoader<TM> la, lb;
-  const int lr = lane & 15;
-  const int c0 = (lane >> 4) ^ (lane & 7);
-  const int offA0 = (wr * 64 + lr) * 128 + (c0 << 4);
-  const int offA1 = (wr * 64 + lr) * 128 + ((c0 ^ 4) << 4);
-  const int offB0 = (wc * 64 + lr) * 128 + (c0 << 4);
-  const int offB1 = (wc * 64 + lr) * 128 + ((c0 ^ 4) << 4);
-  floatx4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int ksteps = K / BK;
-  la.load(Wt, 0, BR, K, 0, tid);
-  lb.load(Xt, 0, BQ, K, 0, tid);
-  la.store(lds, tid);
-  lb.store(lds + BR * 128, tid);
-  __syncthreads();
-  for (int s = 0; s < ksteps; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < ksteps;
-    if (more) {
-      la.load(Wt, 0, BR, K, (s + 1) * BK, tid);
-      lb.load(Xt, 0, BQ, K, (s + 1) * BK, tid);
-    }
-    const char* sa = lds + cur * STAGE_BYTES;
-    const char* sb = sa + BR * 128;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int oa = kk ? offA1 : offA0, ob = kk ? offB1 : offB0;
-      V a[4], bq[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const V*>(sa + oa + m * 16 * 128);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(sb + ob + n * 16 * 128);
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(a[m], bq[n], acc[m][n]);
-    }
-    if (more) {
-      char* st = lds + (cur ^ 1) * STAGE_BYTES;
-      la.store(st, tid);
-      lb.store(st + BR * 128, tid);
-    }
-    __syncthreads();
-  }
-  // epilogue: lane holds features f0 + wr*64 + m*16 + (lane>>4)*4 + r of token t0 + wc*64 + n*16 + lr
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int f = f0 + wr * 64 + m * 16 + (lane >> 4) * 4;
-    if (f >= N_real) continue;          // N_real % 4 == 0 (checked on the host)
-    const float4 bb = *reinterpret_cast<const float4*>(bias + f);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int t = t0 + wc * 64 + n * 16 + lr;
-      if (t >= T_real) continue;
-      float v0 = acc[m][n][0] + bb.x, v1 = acc[m][n][1] + bb.y;
-      float v2 = acc[m][n][2] + bb.z, v3 = acc[m][n][3] + bb.w;
-      if constexpr (EPI == EPI_BIAS_GELU) {
-        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-      }
-      if constexpr (EPI == EPI_BIAS_RESID) {
-        const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
-        float4 o;
-        o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
-        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
-      } else {
-        TM* o = out_h + (size_t)t * ldo + f;
-        o[0] = (TM)v0; o[1] = (TM)v1; o[2] = (TM)v2; o[3] = (TM)v3;
-      }
-    }
-  }
-}
+__device__ __forceinline__ float gelu_exact(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // -------------------------------------------------------------------------------------
 // Self-attention for one (sequence, head): softmax(Q Kᵀ / sqrt(dh) + mask) V.
@@ -491,6 +417,96 @@ size_t attention_mfma_lds(int S) {
   return (((size_t)Sp * (DH + 16) + (size_t)DH * (Sp + 8)) * sizeof(TM) + 15) / 16 * 16 + (size_t)Sp * 4;
 }
 
+
+// -------------------------------------------------------------------------------------
+// fp32 self-attention (reference-precision mode): one workgroup (4 waves) per (sequence,
+// head).  qkv fp32 [T][3H] (q | k | v); K and V of the sequence staged in LDS when they fit
+// (K rows padded to dh + 1 floats: lane-per-key reads are conflict-free), read from L2
+// otherwise.  Scores, softmax (library expf) and P.V in fp32 FMA -- the arithmetic of the
+// torch CPU reference up to summation order; ctx is written as split rows [T][3H].
+// -------------------------------------------------------------------------------------
+__host__ __device__ inline size_t attention_f32_lds(int S, int dh, bool kv_lds) {
+  return ((size_t)5 * S + 4 * dh + (kv_lds ? (size_t)S * (2 * dh + 1) : 0)) * 4;
+}
+
+template <bool KV_LDS>
+__global__ void __launch_bounds__(256)
+attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
+                     int H, int heads, _Float16* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float attf_sm[];
+  const int dh = H / heads;
+  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  const size_t row0 = (size_t)bidx * S;
+  const int ld3 = 3 * H;
+  float* Mk = attf_sm;                    // [S] additive key mask
+  float* Pw = Mk + S;                     // [4 waves][S]
+  float* Qs = Pw + 4 * S;                 // [4 waves][dh]
+  float* Ks = Qs + 4 * dh;                // [S][dh + 1]   (KV_LDS)
+  float* Vs = Ks + (size_t)S * (dh + 1);  // [S][dh]       (KV_LDS)
+  const float* kbase;
+  const float* vbase;
+  int ks, vs;
+  if constexpr (KV_LDS) {
+    for (int i = threadIdx.x; i < S * dh; i += blockDim.x) {
+      const int j = i / dh, d = i - j * dh;
+      const float* base = qkv + (row0 + j) * ld3 + h * dh + d;
+      Ks[(size_t)j * (dh + 1) + d] = base[H];
+      Vs[i] = base[2 * H];
+    }
+    kbase = Ks; ks = dh + 1;
+    vbase = Vs; vs = dh;
+  } else {
+    kbase = qkv + row0 * ld3 + H + h * dh; ks = ld3;
+    vbase = qkv + row0 * ld3 + 2 * H + h * dh; vs = ld3;
+  }
+  for (int j = threadIdx.x; j < S; j += blockDim.x) Mk[j] = mask[row0 + j] ? 0.f : -INFINITY;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float sq = sqrtf((float)dh);      // HF: scores / sqrt(head_size)
+  float* pw = Pw + wave * S;
+  float* qs = Qs + wave * dh;
+  const int G = dh >= 64 ? 1 : 64 / dh;   // key groups in the P.V pass (dh = 32: 2 halves)
+  for (int i = wave; i < S; i += 4) {
+    const float* qrow = qkv + (row0 + i) * ld3 + h * dh;
+    for (int d = lane; d < dh; d += 64) qs[d] = qrow[d];
+    __builtin_amdgcn_wave_barrier();
+    float mx = -INFINITY;
+    for (int j = lane; j < S; j += 64) {
+      const float* kr = kbase + (size_t)j * ks;
+      float acc = 0.f;
+      for (int d = 0; d < dh; ++d) acc = fmaf(qs[d], kr[d], acc);
+      const float sc = acc / sq + Mk[j];
+      pw[j] = sc;
+      mx = fmaxf(mx, sc);
+    }
+    for (int m = 32; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+    float sum = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      const float e = (mx == -INFINITY) ? 0.f : expf(pw[j] - mx);
+      pw[j] = e;
+      sum += e;
+    }
+    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;
+    __builtin_amdgcn_wave_barrier();
+    _Float16* crow = ctx + (row0 + i) * ld3;
+    if (G == 1) {
+      for (int d = lane; d < dh; d += 64) {
+        float o = 0.f;
+        for (int j = 0; j < S; ++j) o = fmaf(pw[j], vbase[(size_t)j * vs + d], o);
+        store_act1<_Float16, true>(crow, H, h * dh + d, o * inv);
+      }
+    } else {
+      const int d = lane % dh, grp = lane / dh;
+      float o = 0.f;
+      for (int j = grp; j < S; j += G) o = fmaf(pw[j], vbase[(size_t)j * vs + d], o);
+      for (int m = dh; m < 64; m <<= 1) o += __shfl_xor(o, m, 64);
+      if (grp == 0) store_act1<_Float16, true>(crow, H, h * dh + d, o * inv);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // -------------------------------------------------------------------------------------
 // Pooling + L2 normalise (one block per sequence).
 //   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
@@ -529,6 +545,23 @@ pool_normalize_kernel(const float* __restrict__ x, const int32_t* __restrict__ m
   if (!normalize) return;
   const float nrm = fmaxf(sqrtf(red[0]), 1e-12f);
   for (int d = threadIdx.x; d < H; d += blockDim.x) out[(size_t)bidx * H + d] /= nrm;
+}
+
+// Reference-precision weights: W [rows][cols] fp32 (times the power-of-two `scale` that puts
+// max |W| near 16) -> [rows_pad][3 cols] f16 = [Wh * 2^11 | Wl * 2^11 | Wh] with Wh = f16(W),
+// Wl = W - Wh (see store_act4); rows past `rows` are zero.
+__global__ void to_split_weights(const float* __restrict__ src, int64_t rows, int64_t rows_pad,
+                                 int cols, float scale, _Float16* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_pad * cols) return;
+  const int64_t r = i / cols;
+  const int c = (int)(i - r * cols);
+  const float w = r < rows ? src[i] * scale : 0.f;
+  const _Float16 hi = (_Float16)w;
+  _Float16* o = dst + r * 3 * cols;
+  o[c] = (_Float16)((float)hi * kSplitLo);
+  o[cols + c] = (_Float16)((w - (float)hi) * kSplitLo);
+  o[2 * cols + c] = hi;
 }
 
 // fp32 -> MFMA dtype conversion with zero padding of rows [rows, rows_pad)

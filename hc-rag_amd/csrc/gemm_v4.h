@@ -1,6 +1,11 @@
 // gemm_v4.h — encoder projection GEMM on the LDS-DMA ring of the v4 score kernel
 // (score_v4.h): C[token][feature] = X[token][:] · W[feature][:] + bias (+ GELU | + residual).
 //
+// Reference-precision mode: X = [Xh | Xh | Xl*2^11] and W = [Wh*2^11 | Wl*2^11 | Wh] (K = 3 x
+// the model width, encoder_kernels.h store_act4 / to_split_weights) make the same kernel
+// compute 2^11 (Xh Wh + Xh Wl + Xl Wh); `oscale` undoes that factor and the weights' power-of-
+// two scale (1 in the fast modes: fma(acc, 1, bias) = acc + bias exactly).
+//
 // One workgroup = one 256-feature x 256-token output tile over the whole K; 8 waves (2 x 4),
 // each 128 features x 64 tokens as 8 x 4 16x16x32 MFMA blocks; K = 32 per stage, NST-stage
 // LDS-DMA ring with the 4 DMA pieces of stage s + NST - 1 interleaved between the MFMA groups
@@ -23,7 +28,7 @@ template <typename TM, int EPI, int NST, int FT>
 __global__ void __launch_bounds__(V3_NT, 2)
 gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_real, int T_real,
                int n_tiles_feat, const float* __restrict__ bias, const float* __restrict__ resid,
-               TM* __restrict__ out_h, float* __restrict__ out_f, int ldo) {
+               TM* __restrict__ out_h, float* __restrict__ out_f, int ldo, float oscale) {
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   static_assert(FT == 256 || FT == 192, "feature tile");
@@ -151,19 +156,23 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
     for (int n = 0; n < NQ; ++n) {
       const int t = t0 + wn * 64 + n * 16 + (lane & 15);
       if (t >= T_real) continue;
-      float v0 = acc[m][n][0] + bb.x, v1 = acc[m][n][1] + bb.y;
-      float v2 = acc[m][n][2] + bb.z, v3 = acc[m][n][3] + bb.w;
+      float v0 = fmaf(acc[m][n][0], oscale, bb.x), v1 = fmaf(acc[m][n][1], oscale, bb.y);
+      float v2 = fmaf(acc[m][n][2], oscale, bb.z), v3 = fmaf(acc[m][n][3], oscale, bb.w);
       if constexpr (EPI == EPI_BIAS_GELU) {
         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
       }
-      if constexpr (EPI == EPI_BIAS_RESID) {
+      if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
+        v0 = gelu_exact(v0); v1 = gelu_exact(v1); v2 = gelu_exact(v2); v3 = gelu_exact(v3);
+        store_act4<TM, true>(out_h + (size_t)t * 3 * ldo, ldo, f, float4{v0, v1, v2, v3});
+      } else if constexpr (EPI == EPI_BIAS_RESID) {
         const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
         float4 o;
         o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
         *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
+      } else if constexpr (EPI == EPI_BIAS_F32) {
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = float4{v0, v1, v2, v3};
       } else {
-        TM* o = out_h + (size_t)t * ldo + f;
-        o[0] = (TM)v0; o[1] = (TM)v1; o[2] = (TM)v2; o[3] = (TM)v3;
+        store_act4<TM, false>(out_h + (size_t)t * ldo, ldo, f, float4{v0, v1, v2, v3});
       }
     }
   }

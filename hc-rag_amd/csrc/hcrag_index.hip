@@ -22,7 +22,6 @@
 #include "topk_kernels.h"
 #include "score_v3.h"
 #include "score_v4.h"
-#include "score_v5.h"
 
 using namespace hcr;
 
@@ -63,6 +62,8 @@ struct hcr_index {
   int64_t cap = 0;      // allocated rows (multiple of 128)
   int64_t id_offset = 0;
   DevBuf rows, norm64, inv32, maskbits, rho;
+  DevBuf idmap;                 // int64 global id per row (only once hcr_index_add_ids was used)
+  bool has_idmap = false;
   bool has_mask = false;
   bool rho_dirty = true;
   double rho_host = 0.0;
@@ -70,11 +71,25 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt, w_tauest, w_umax;
+      w_unc, w_cnt, w_tauest, w_umax, w_sk;
+  // exact fallback workspace (K6/K7)
+  DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again;
   hcr_search_stats stats{};
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
+  // anything reads the rows, norms or rho
+  hipEvent_t ev_ingest = nullptr;
+  bool ingest_pending = false;
 };
+
+// Host-side wait for the last device ingest (ordering against the caller's stream).
+static int wait_ingest(hcr_index* ix) {
+  if (!ix->ingest_pending) return HCR_OK;
+  HIPC(hipEventSynchronize(ix->ev_ingest));
+  ix->ingest_pending = false;
+  return HCR_OK;
+}
 
 static size_t dtype_size(int dt) { return dt == HCR_F32 ? 4 : 2; }
 static constexpr int64_t kSlackRows = 512;
@@ -125,11 +140,14 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
   if (!ix) return HCR_OK;
   (void)hipSetDevice(ix->device);
   if (ix->stream) (void)hipStreamSynchronize(ix->stream);
-  DevBuf* all[] = {&ix->rows, &ix->norm64, &ix->inv32, &ix->maskbits, &ix->rho,
+  DevBuf* all[] = {&ix->rows, &ix->norm64, &ix->inv32, &ix->maskbits, &ix->rho, &ix->idmap,
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
-                   &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax};
+                   &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax, &ix->w_sk,
+                   &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
+                   &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again};
   for (DevBuf* b : all) b->release();
+  if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
   if (ix->ev1) (void)hipEventDestroy(ix->ev1);
   if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -140,9 +158,11 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
 extern "C" int hcr_index_reset(hcr_index* ix) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
   HIPC(hipStreamSynchronize(ix->stream));
   ix->n = 0;
   ix->has_mask = false;
+  ix->has_idmap = false;
   ix->rho_dirty = true;
   // on the index stream: a null-stream memset does not order against it
   HIPC(hipMemsetAsync(ix->rho.p, 0, 16, ix->stream));
@@ -153,14 +173,16 @@ extern "C" int hcr_index_reset(hcr_index* ix) {
 
 static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows) {
   if (want_rows <= ix->cap) return HCR_OK;
+  CHECK(wait_ingest(ix));        // the copy below reads rows a device ingest may still write
   int64_t ncap = std::max<int64_t>(want_rows, ix->cap + ix->cap / 2);
   ncap = round_up(std::max<int64_t>(ncap, 256), 256);
   // kSlackRows past the capacity: the score kernels read whole tiles (and DMA whole 1 KiB
   // inverse-norm slots), so every allocation covers the last tile plus slack.
   const int64_t arows = ncap + kSlackRows;
   const size_t es = dtype_size(ix->dtype);
-  DevBuf nrows, nn64, ninv, nmask;
+  DevBuf nrows, nn64, ninv, nmask, nidm;
   CHECK(nrows.ensure((size_t)arows * ix->ld * es));
+  if (ix->has_idmap) CHECK(nidm.ensure((size_t)arows * 8));
   CHECK(nn64.ensure((size_t)arows * 8));
   CHECK(ninv.ensure((size_t)arows * 4));
   CHECK(nmask.ensure((size_t)(arows / 32) * 4));
@@ -173,11 +195,18 @@ static int hcr_reserve_internal(hcr_index* ix, int64_t want_rows) {
     HIPC(hipMemcpyAsync(ninv.p, ix->inv32.p, (size_t)ix->n * 4, hipMemcpyDeviceToDevice, ix->stream));
     if (ix->has_mask)
       HIPC(hipMemcpyAsync(nmask.p, ix->maskbits.p, (size_t)(ix->cap / 32) * 4, hipMemcpyDeviceToDevice, ix->stream));
+    if (ix->has_idmap)
+      HIPC(hipMemcpyAsync(nidm.p, ix->idmap.p, (size_t)ix->n * 8, hipMemcpyDeviceToDevice, ix->stream));
   }
   HIPC(hipStreamSynchronize(ix->stream));
   ix->rows.release(); ix->norm64.release(); ix->inv32.release(); ix->maskbits.release();
   ix->rows = nrows; ix->norm64 = nn64; ix->inv32 = ninv; ix->maskbits = nmask;
   nrows.p = nn64.p = ninv.p = nmask.p = nullptr;   // ownership moved
+  if (ix->has_idmap) {
+    ix->idmap.release();
+    ix->idmap = nidm;
+    nidm.p = nullptr;
+  }
   ix->cap = ncap;
   return HCR_OK;
 }
@@ -208,6 +237,11 @@ static int ingest_device(hcr_index* ix, const void* d_rows, int64_t n, int in_dt
   }
 #undef ING
   HIPC(hipGetLastError());
+  if (ix->has_idmap) {            // plain adds after id-mapped ones: id_offset + row
+    hipLaunchKernelGGL(iota_ids_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       ix->idmap.as<int64_t>() + ix->n, n, ix->id_offset + ix->n);
+    HIPC(hipGetLastError());
+  }
   ix->n += n;
   ix->rho_dirty = true;
   return HCR_OK;
@@ -226,7 +260,14 @@ extern "C" int hcr_index_add_device(hcr_index* ix, const void* d_rows, int64_t n
   // it (e.g. torch's default stream producing the input) is ordered before ours
   hipStream_t st = (hipStream_t)stream;
   if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
-  return ingest_device(ix, d_rows, n, rows_dtype, normalize, st);
+  CHECK(ingest_device(ix, d_rows, n, rows_dtype, normalize, st));
+  if (st != ix->stream) {
+    // later reads of the rows / norms / rho (search, reserve, get_rows) wait for this event
+    if (!ix->ev_ingest) HIPC(hipEventCreateWithFlags(&ix->ev_ingest, hipEventDisableTiming));
+    HIPC(hipEventRecord(ix->ev_ingest, st));
+    ix->ingest_pending = true;
+  }
+  return HCR_OK;
 }
 
 extern "C" int hcr_index_add(hcr_index* ix, const void* rows, int64_t n, int rows_dtype,
@@ -249,6 +290,33 @@ extern "C" int hcr_index_add(hcr_index* ix, const void* rows, int64_t n, int row
                         hipMemcpyHostToDevice, ix->stream));
     CHECK(ingest_device(ix, ix->w_qin.p, m, rows_dtype, normalize, ix->stream));
   }
+  HIPC(hipStreamSynchronize(ix->stream));
+  return HCR_OK;
+}
+
+extern "C" int hcr_index_add_ids(hcr_index* ix, const void* rows, int64_t n, int rows_dtype,
+                                 int normalize, const int64_t* ids) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (n < 0) return set_err(HCR_EINVAL, "negative row count");
+  if (n == 0) return HCR_OK;
+  if (!ids) return set_err(HCR_EINVAL, "ids is NULL");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
+  const int64_t n0 = ix->n;
+  CHECK(hcr_reserve_internal(ix, n0 + n));
+  if (!ix->has_idmap) {           // first id-mapped add: the existing rows keep their ids
+    CHECK(ix->idmap.ensure((size_t)(ix->cap + kSlackRows) * 8));
+    if (n0 > 0) {
+      hipLaunchKernelGGL(iota_ids_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0,
+                         ix->stream, ix->idmap.as<int64_t>(), n0, ix->id_offset);
+      HIPC(hipGetLastError());
+    }
+    ix->has_idmap = true;
+  }
+  CHECK(hcr_index_add(ix, rows, n, rows_dtype, normalize));
+  // the plain add above wrote id_offset + row for the new rows; overwrite with the given ids
+  HIPC(hipMemcpyAsync(ix->idmap.as<int64_t>() + n0, ids, (size_t)n * 8, hipMemcpyHostToDevice,
+                      ix->stream));
   HIPC(hipStreamSynchronize(ix->stream));
   return HCR_OK;
 }
@@ -291,6 +359,7 @@ extern "C" int hcr_index_get_rows(const hcr_index* ix, int64_t row0, int64_t n, 
   if (row0 < 0 || n < 0 || row0 + n > ix->n) return set_err(HCR_EINVAL, "row range out of bounds");
   if (n == 0) return HCR_OK;
   HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(const_cast<hcr_index*>(ix)));
   const size_t es = dtype_size(ix->dtype);
   std::vector<char> tmp((size_t)n * ix->ld * es);
   HIPC(hipStreamSynchronize(ix->stream));
@@ -319,9 +388,12 @@ extern "C" int hcr_index_set_rowmask(hcr_index* ix, const uint8_t* mask, int64_t
   if (!mask) { ix->has_mask = false; return HCR_OK; }
   if (n != ix->n) return set_err(HCR_EINVAL, "mask length %lld != index size %lld", (long long)n, (long long)ix->n);
   if (ix->cap == 0) { ix->has_mask = false; return HCR_OK; }
-  std::vector<uint32_t> bits((size_t)((ix->cap + kSlackRows) / 32), 0u);
+  CHECK(wait_ingest(ix));
+  // rows appended after the mask is set are visible (their bits are 1, as in a fresh or
+  // regrown allocation); rows past the size are never scored either way
+  std::vector<uint32_t> bits((size_t)((ix->cap + kSlackRows) / 32), 0xFFFFFFFFu);
   for (int64_t i = 0; i < n; ++i)
-    if (mask[i]) bits[(size_t)(i >> 5)] |= 1u << (i & 31);
+    if (!mask[i]) bits[(size_t)(i >> 5)] &= ~(1u << (i & 31));
   HIPC(hipMemcpyAsync(ix->maskbits.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ix->stream));
   HIPC(hipStreamSynchronize(ix->stream));
   ix->has_mask = true;
@@ -352,7 +424,6 @@ static int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 static constexpr int kMaxKprime = 512;
 static constexpr int kMergeMaxKeys = 8192;      // 64 KiB of LDS in merge_partials_kernel
 static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
-static int kV2MinQueries = 384;                 // batch size from which K2 v2 is used
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
 
@@ -378,28 +449,39 @@ static int dispatch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, int
   return HCR_OK;
 }
 
-template <typename TM, int CAP>
-static void launch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk224_kernel<TM, CAP>), dim3(nqb * P), dim3(NT2), 0, st,
-                     ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / BK, ix->inv32.as<const float>(),
-                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
-                     ix->w_qhat.as<const TM>(), nqb, P, ntiles, ix->w_buf.as<uint64_t>(),
-                     ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), kp);
-}
-
-template <typename TM>
-static int dispatch_score256(hcr_index* ix, int nqb, int P, int ntiles, int kp, int cap, hipStream_t st) {
-  switch (cap) {
-    case 512: launch_score256<TM, 512>(ix, nqb, P, ntiles, kp, st); break;
-    case 1024: launch_score256<TM, 1024>(ix, nqb, P, ntiles, kp, st); break;
-    default: return set_err(HCR_EINVAL, "internal: unsupported candidate capacity %d", cap);
-  }
-  HIPC(hipGetLastError());
-  return HCR_OK;
-}
-
 // ---- K2 v3 (score_v3.h): tile configurations by batch size ----
 static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_cfg
+
+// Test hooks, read once per process.  They force paths the default heuristics only take at
+// scale (or rarely) so that the parity tests reach them on small corpora; they never change
+// results, only which exact path produces them.
+//   HCRAG_Q64_ELEMS         corpus-size threshold of the 256 x 64 tiles (17-64 queries)
+//   HCRAG_NO_PREPASS        no sampling pre-pass (cold per-workgroup bounds)
+//   HCRAG_PREPASS_MIN_TILES dense tiles per workgroup from which the pre-pass runs
+//   HCRAG_SAMPLE_STRIDE     pre-pass sampling stride
+//   HCRAG_RIGOROUS_SEED     seed rank j = k' (rigorous) instead of the estimate
+//   HCRAG_SEED_RANK         force seed rank j (aggressive seeds exercise the re-runs)
+//   HCRAG_PREPASS_TOPK      the top-k' pre-pass form instead of MAXONLY
+struct TestHooks {
+  int64_t q64_elems = kQ64WideMaxElems;
+  bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
+  int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
+};
+static const TestHooks& hooks() {
+  static const TestHooks h = [] {
+    TestHooks t;
+    if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
+    t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
+    t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
+    t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
+    if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
+    if (const char* e = getenv("HCRAG_SAMPLE_STRIDE")) t.sample_stride = std::max(2, atoi(e));
+    if (const char* e = getenv("HCRAG_SEED_RANK")) t.seed_rank = std::max(1, atoi(e));
+    return t;
+  }();
+  return h;
+}
+
 struct V3Cfg { int rt, qt, nst; };
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
   if (nq <= 16) return {256, 16, 8};
@@ -407,21 +489,13 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
   // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
   // 1M x 768 0.49 vs 0.52, 2.5M x 768 1.11 vs 1.08, 5M x 768 2.13 vs 1.98, 10M x 768 4.13 vs
   // 3.73 -> the crossover is between 0.8e9 and 1.9e9 corpus elements (the cost of either tile
-  // shape is flat in the batch within its range).  HCRAG_Q64_ELEMS overrides it.
-  static const int64_t q64_elems = [] {
-    const char* e = getenv("HCRAG_Q64_ELEMS");
-    return e ? (int64_t)atoll(e) : kQ64WideMaxElems;
-  }();
-  if (nq <= 64 && n_rows * (int64_t)ld <= q64_elems) return {256, 256, 4};
+  // shape is flat in the batch within its range).
+  if (nq <= 64 && n_rows * (int64_t)ld <= hooks().q64_elems) return {256, 256, 4};
   if (nq <= 64) return {256, 64, 7};
-  // 65-128 queries: the 256 x 256 kernel (half its query columns padded, MAXONLY pre-pass,
-  // UNIT epilogue) beats 256 x 128 (r01g sweeps: 10M x 768 B = 200 4.51 ms vs B = 128 4.74 ms
-  // on 256 x 128; 1M x 384 0.31 vs 0.57 ms).  HCRAG_QT128=1 keeps 256 x 128 for A/B.
-  static const bool qt128 = getenv("HCRAG_QT128") != nullptr;
-  if (nq <= 128 && qt128) return {256, 128, 6};
-  // large batches: v4 (256 x 256, NST 4) unless HCRAG_V3_LARGE=1 keeps v3's 224 x 256
-  static const bool v3_large = getenv("HCRAG_V3_LARGE") != nullptr;
-  return v3_large ? V3Cfg{224, 256, 5} : V3Cfg{256, 256, 4};
+  // 65+ queries: the 256 x 256 kernel (v4), also for 65-128 where half its query columns are
+  // padding (MAXONLY pre-pass + UNIT epilogue; r01g sweeps: 10M x 768 B = 200 4.51 ms vs
+  // B = 128 4.74 ms on 256 x 128; 1M x 384 0.31 vs 0.57 ms)
+  return V3Cfg{256, 256, 4};
 }
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
@@ -457,27 +531,7 @@ static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
 
 template <typename TM, int CAP>
 static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
-  // v5 (score_v5.h) is an experiment kept for A/B: HCRAG_V5=1.  It measured ~5 % slower than
-  // v4 in situ (profiles/r01b/v5_ablation.txt); v4 stays the default.
-  static const bool use_v5 = getenv("HCRAG_V5") != nullptr;
-  if (c.qt == 256 && c.rt == 256 && use_v5) {
-    if (a.unit)
-      hipLaunchKernelGGL((score_topk_v5_kernel<TM, CAP, 4, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
-                         ix->inv32.as<const float>(),
-                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
-                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
-                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                         ix->w_part.as<uint64_t>(), a.kp);
-    else
-      hipLaunchKernelGGL((score_topk_v5_kernel<TM, CAP, 4, false>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                         ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
-                         ix->inv32.as<const float>(),
-                         ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
-                         ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
-                         ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                         ix->w_part.as<uint64_t>(), a.kp);
-  } else if (c.qt == 256 && c.rt == 256) {
+  if (c.qt == 256) {
     if (a.unit)
       hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                          ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
@@ -495,8 +549,6 @@ static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
                          ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
                          ix->w_part.as<uint64_t>(), a.kp);
   }
-  else if (c.qt == 256) launch_v3_t<TM, CAP, 224, 256, 2, 4, 5>(ix, a, st);
-  else if (c.qt == 128) launch_v3_t<TM, CAP, 256, 128, 4, 2, 6>(ix, a, st);
   else if (c.qt == 64) launch_v3_t<TM, CAP, 256, 64, 4, 2, 7>(ix, a, st);
   else launch_v3_t<TM, CAP, 256, 16, 8, 1, 8>(ix, a, st);
   HIPC(hipGetLastError());
@@ -541,7 +593,8 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
                      ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
-                     ix->w_tauest.as<const uint32_t>());
+                     ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
 }
 
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
@@ -616,22 +669,12 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                        double* d_out_s, int64_t* d_out_i, int kp, hipStream_t st, int* n_unc,
                        std::vector<int>* unc_list, bool rigorous_seed = false) {
   const uint64_t* merged_ptr = nullptr;
-  // kernel choice (HCRAG_SCORE_KERNEL=v1|v2|v3 overrides): v3 (deep LDS-DMA ring, tile shape
-  // by batch size) for 16-bit rows; v1 (register-staged 128 x 128, converts fp32 rows to
-  // bf16 on the way into LDS) for fp32 rows.
-  static const int forced = [] {
-    const char* e = getenv("HCRAG_SCORE_KERNEL");
-    if (getenv("HCRAG_DISABLE_V2")) return 1;
-    if (!e) return 0;
-    return e[0] == 'v' ? atoi(e + 1) : 0;
-  }();
-  int ver = ix->dtype == HCR_F32 ? 1 : (forced ? forced : 3);
-  if (ver == 2 && nq < kV2MinQueries) ver = 1;
-  if (ix->dtype == HCR_F32) ver = 1;
+  // kernel choice: v3/v4 (deep LDS-DMA ring, tile shape by batch size) for 16-bit rows;
+  // v1 (register-staged 128 x 128, converts fp32 rows to bf16 on the way into LDS) for fp32
+  // rows and for rows too narrow for the v3 tile-slot rings.
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld);
-  if (ver == 3 && !v3_fits(ix, c3)) ver = 1;
-  const bool v2 = ver == 2;
-  const int tq = ver == 3 ? c3.qt : v2 ? Q2 : BQ, tr = ver == 3 ? c3.rt : v2 ? R2 : BR;
+  const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
+  const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
   const int nqpad = (int)round_up(nq, tq);
   const int nqb = nqpad / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
@@ -655,17 +698,14 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_unc.ensure((size_t)nqpad * 4));
   CHECK(ix->w_cnt.ensure(16));
   CHECK(ix->w_tauest.ensure((size_t)nqpad * 4));
+  CHECK(ix->w_sk.ensure((size_t)nqpad * 8));
 
   HIPC(hipMemsetAsync(ix->w_qhat.p, 0, (size_t)nqpad * ix->ld * tms, st));
-  // HCRAG_DEBUG_KEEP_TAUG (diagnostic only): keep the per-query bound of the previous search
-  // and skip the pre-pass -- a repeated identical batch then runs with the final bound
-  static const bool keep_taug = getenv("HCRAG_DEBUG_KEEP_TAUG") != nullptr;
-  if (!keep_taug) HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
+  HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
   // Padded query columns (q^ = 0, every score 0) get the bound ord32(+inf): with bound 0 they
   // passed the epilogue's tile test on every tile and sent their waves down the exact path
   // (r01g: B = 1 on the 256 x 16 tiles slower than B = 16).  Nothing reads their lists.
-  static const bool no_pad_bound = getenv("HCRAG_NO_PAD_BOUND") != nullptr;   // A/B switch
-  if (!keep_taug && !no_pad_bound && nqpad > nq)
+  if (nqpad > nq)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ix->w_taug.as<uint32_t>() + nq),
                            (int)0xFF800000u, (size_t)(nqpad - nq), st));
   HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
@@ -696,14 +736,8 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double rho = ix->rho_host;
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
-  static const bool no_unit = getenv("HCRAG_NO_UNIT") != nullptr;
-  const bool unit = !no_unit && ver == 3 && c3.rt == 256 && c3.qt == 256 &&
-                    ix->unit_dev_host <= kUnitDevMax;
+  const bool unit = ver == 3 && c3.rt == 256 && c3.qt == 256 && ix->unit_dev_host <= kUnitDevMax;
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
-  static const bool dbg_unit = getenv("HCRAG_DEBUG_UNIT") != nullptr;
-  if (dbg_unit)
-    fprintf(stderr, "[hcrag] unit=%d ver=%d rt=%d qt=%d unit_dev=%.3e rho=%.3e nq=%d\n", (int)unit,
-            ver, c3.rt, c3.qt, ix->unit_dev_host, rho, nq);
   ix->stats.unit_kernel = unit ? 1 : 0;
 
   const unsigned gq = (unsigned)((nq + 3) / 4);
@@ -722,36 +756,20 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     // Sampling pre-pass (every kSampleStride-th row tile): the k'-th best coarse key of the
     // sample is <= the global k'-th best coarse key, so it seeds the per-query global bound
     // tau_g exactly; the dense pass then appends only rows that can still be in the top-k'.
-    static const bool no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
-    static const int min_tiles = [] {    // HCRAG_PREPASS_MIN_TILES: tests force the pre-pass
-      const char* e = getenv("HCRAG_PREPASS_MIN_TILES");
-      return e ? std::max(1, atoi(e)) : kPrepassMinTilesPerWg;
-    }();
-    static const int kSampleStrideEnv = [] {   // HCRAG_SAMPLE_STRIDE: pre-pass sampling stride
-      const char* e = getenv("HCRAG_SAMPLE_STRIDE");
-      return e ? std::max(2, atoi(e)) : 0;
-    }();
-    if (!no_prepass && !keep_taug && ntiles >= (int64_t)P * min_tiles) {
+    const TestHooks& th = hooks();
+    const int min_tiles = th.prepass_min_tiles ? th.prepass_min_tiles : kPrepassMinTilesPerWg;
+    if (!th.no_prepass && ntiles >= (int64_t)P * min_tiles) {
       // Seed rank j.  j = k' is rigorous (k' real rows at or above the seed); a smaller j
       // estimates the global k'-th best much more tightly (the sample holds lambda = k' x
       // sampled fraction of the global top-k' on average, Poisson): j = lambda + 5 sqrt(lambda)
       // + 3 leaves fewer than k' rows above the seed with probability ~1e-6 per query, and the
       // certificate then counts the seed as the bound of the excluded rows, so such a query is
-      // re-run (widened, rigorous seed) instead of answered wrong.  HCRAG_RIGOROUS_SEED=1 keeps
-      // j = k'; HCRAG_SEED_RANK=j forces j (tests: an aggressive seed exercises the widened
-      // certificate and the re-run).
-      static const bool rigorous_env = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
-      static const int forced_rank = [] {
-        const char* e = getenv("HCRAG_SEED_RANK");
-        return e ? std::max(1, atoi(e)) : 0;
-      }();
+      // re-run (widened, rigorous seed, exact fallback) instead of answered wrong.
       // Two pre-pass forms: MAXONLY (default for the 256 x 256 kernel: the largest score of
       // every sampled 128-row unit per query, no candidate lists, stride 64) and the top-k'
-      // form (every sampled row a candidate, merged; stride 512; HCRAG_PREPASS_TOPK=1 or the
-      // other tile shapes).
-      static const bool topk_env = getenv("HCRAG_PREPASS_TOPK") != nullptr;
-      const bool maxonly = !topk_env && c3.rt == 256 && c3.qt == 256;
-      int stride = kSampleStrideEnv > 0 ? kSampleStrideEnv
+      // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
+      const bool maxonly = !th.prepass_topk && c3.rt == 256 && c3.qt == 256;
+      int stride = th.sample_stride > 0 ? th.sample_stride
                                         : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;
       if (maxonly) stride = std::max<int>(stride, (int)((2 * ntiles + kMaxUnits - 1) / kMaxUnits));
@@ -759,9 +777,9 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
       a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
       int j = kp;
-      if (!rigorous_seed && !rigorous_env) {
+      if (!rigorous_seed && !th.rigorous_seed) {
         const double lam = (double)kp * ((double)a.nvt * tr) / (double)ix->n;
-        j = forced_rank ? forced_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
+        j = th.seed_rank ? th.seed_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
         j = std::min(kp, std::max(1, j));
       }
       if (maxonly) {
@@ -788,41 +806,18 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     const V3Launch a{nqb, P, (int)ntiles, 1, kp, unit};
     if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
     else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
-  } else if (v2) {
-    if (ix->dtype == HCR_F16) CHECK((dispatch_score256<_Float16>(ix, nqb, P, ntiles, kp, cap, st)));
-    else CHECK((dispatch_score256<__bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   } else if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
   else if (ix->dtype == HCR_BF16) CHECK((dispatch_score<__bf16, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
   CHECK(merge_tree(ix, nq, nqpad, P, P2, G, kp, st, &merged_ptr));
-  // HCRAG_DEBUG_ORACLE_TAU=r (diagnostic only, with HCRAG_DEBUG_KEEP_TAUG): seed the next
-  // search's bound with this search's r-th best coarse key -- the bound a perfect seeding
-  // would give, to price the dense pass's append path
-  static const int oracle_rank = [] {
-    const char* e = getenv("HCRAG_DEBUG_ORACLE_TAU");
-    return e ? atoi(e) : 0;
-  }();
-  if (oracle_rank > 0 && ver == 3)
-    hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
-                       merged_ptr, nq, kp, ix->w_taug.as<uint32_t>(), std::min(oracle_rank, kp));
 
   if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else launch_rescore<float>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   HIPC(hipGetLastError());
 
-#ifdef HCR_V4_COUNT
-  {   // diagnostic build: v4 epilogue event counts of this pass (stderr)
-    unsigned long long h[4], z[4] = {0, 0, 0, 0};
-    HIPC(hipStreamSynchronize(st));
-    HIPC(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_v4_count), sizeof(h)));
-    HIPC(hipMemcpyToSymbol(HIP_SYMBOL(g_v4_count), z, sizeof(z)));
-    fprintf(stderr, "[v4count] nq=%d slow=%llu appends=%llu epilogues=%llu compactions=%llu\n", nq,
-            h[0], h[1], h[2], h[3]);
-  }
-#endif
   int cnt = 0;
   HIPC(hipMemcpyAsync(&cnt, ix->w_cnt.p, 4, hipMemcpyDeviceToHost, st));
   HIPC(hipStreamSynchronize(st));
@@ -847,7 +842,80 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   return HCR_OK;
 }
 
-// Full search of nq device queries with certificate widening.
+// ---- exact fallback (K6 + K7, topk_kernels.h) ----
+static constexpr int kFallbackCap = 8192;     // buffer slots per query (LDS sort of 2 x 64 KiB)
+static constexpr int kFallbackGroup = 32;     // queries per row scan
+static constexpr int kFallbackMaxRounds = 64; // each round strictly raises the threshold key
+static constexpr int kMaxFastK = 256;         // k' = 2k <= 512: larger k go straight to K6/K7
+static constexpr int kMaxK = 2048;            // kFallbackCap > k: every K7 round makes progress
+
+// Exact top-k of the chunk-local queries `idx` of the m x dim device queries `qc` by one fp64
+// scan of every row (a K6/K7 round per threshold); results go to rows idx[i] of os / oi.
+// sk[i]: the starting threshold (K4's s_k of the candidates; 0 = every row).
+static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>& idx,
+                          const std::vector<uint64_t>& sk, int k, int mode, double thr, double* os,
+                          int64_t* oi, hipStream_t st) {
+  const int cap = kFallbackCap;
+  const size_t sel_lds = (size_t)2 * cap * 8;
+  HIPC(hipFuncSetAttribute((const void*)exact_select_kernel,
+                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+  for (size_t g0 = 0; g0 < idx.size(); g0 += kFallbackGroup) {
+    const int ng = (int)std::min<size_t>(kFallbackGroup, idx.size() - g0);
+    CHECK(ix->f_idx.ensure((size_t)ng * 4));
+    CHECK(ix->f_q.ensure((size_t)ng * ix->dim * 4));
+    CHECK(ix->f_qn.ensure((size_t)ng * 8));
+    CHECK(ix->f_thh.ensure((size_t)ng * 8));
+    CHECK(ix->f_thl.ensure((size_t)ng * 8));
+    CHECK(ix->f_act.ensure((size_t)ng * 4));
+    CHECK(ix->f_cnt.ensure((size_t)ng * 4));
+    CHECK(ix->f_bufh.ensure((size_t)ng * cap * 8));
+    CHECK(ix->f_bufl.ensure((size_t)ng * cap * 8));
+    CHECK(ix->f_again.ensure(16));
+    std::vector<uint64_t> thh(sk.begin() + g0, sk.begin() + g0 + ng), thl(ng, 0ull);
+    std::vector<int> act(ng, 1);
+    HIPC(hipMemcpyAsync(ix->f_idx.p, idx.data() + g0, (size_t)ng * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(ix->f_thl.p, thl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(ix->f_act.p, act.data(), (size_t)ng * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(gather_rows_f32, dim3(ng), dim3(256), 0, st, qc, ix->f_idx.as<const int>(), ng,
+                       ix->dim, ix->f_q.as<float>());
+    hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
+                       ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
+    HIPC(hipGetLastError());
+    const unsigned fgrid = (unsigned)std::min<int64_t>((ix->n + 3) / 4, 8192);
+    int again = 1, rounds = 0;
+    while (again > 0) {
+      if (++rounds > kFallbackMaxRounds)
+        return set_err(HCR_EHIP, "internal: exact fallback did not converge in %d rounds", kFallbackMaxRounds);
+      HIPC(hipMemsetAsync(ix->f_cnt.p, 0, (size_t)ng * 4, st));
+      HIPC(hipMemsetAsync(ix->f_again.p, 0, 4, st));
+#define FIL(TS)                                                                                  \
+  hipLaunchKernelGGL((exact_filter_kernel<TS>), dim3(fgrid), dim3(256), 0, st,                  \
+                     ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<const double>(),       \
+                     ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(),     \
+                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,                \
+                     ix->f_thh.as<const uint64_t>(), ix->f_thl.as<const uint64_t>(),            \
+                     ix->f_act.as<const int>(), cap, ix->f_cnt.as<unsigned int>(),               \
+                     ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>())
+      if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
+#undef FIL
+      hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
+                         ix->f_cnt.as<const unsigned int>(), ix->f_bufh.as<const uint64_t>(),
+                         ix->f_bufl.as<const uint64_t>(), ix->f_thh.as<uint64_t>(),
+                         ix->f_thl.as<uint64_t>(), ix->f_act.as<int>(), ix->f_again.as<int>(), mode,
+                         thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
+                         ix->f_idx.as<const int>(), os, oi);
+      HIPC(hipGetLastError());
+      HIPC(hipMemcpyAsync(&again, ix->f_again.p, 4, hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+    }
+    ix->stats.fallback_rounds += rounds;
+  }
+  return HCR_OK;
+}
+
+// Full search of nq device queries: certified top-k (K1-K4), certificate widening, and the
+// exact fallback for whatever is still uncertified -- every returned list is the exact top-k.
 static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k, int mode,
                               double thr, double* d_out_s, int64_t* d_out_i, hipStream_t st) {
   ix->stats = hcr_search_stats{};
@@ -860,16 +928,32 @@ static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k
     HIPC(hipStreamSynchronize(st));
     return HCR_OK;
   }
-  const int kp0 = choose_kprime(k);
-  ix->stats.kprime = kp0;
+  const int kp0 = choose_kprime(std::min(k, kMaxFastK));
+  ix->stats.kprime = k > kMaxFastK ? 0 : kp0;
   for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
     const int m = (int)std::min<int64_t>(kQueryChunk, nq - q0);
     const float* qc = d_q + q0 * ix->dim;
     double* os = d_out_s + q0 * k;
     int64_t* oi = d_out_i + q0 * k;
+    if (k > kMaxFastK) {            // no MFMA candidate path this deep: exact scan
+      std::vector<int> all(m);
+      for (int i = 0; i < m; ++i) all[i] = i;
+      CHECK(exact_fallback(ix, qc, all, std::vector<uint64_t>(m, 0ull), k, mode, thr, os, oi, st));
+      ix->stats.fallback_queries += m;
+      continue;
+    }
     int n_unc = 0;
     std::vector<int> unc;
     CHECK(search_pass(ix, qc, m, k, mode, thr, os, oi, kp0, st, &n_unc, &unc));
+    std::vector<uint64_t> sk_chunk;     // K4's s_k per chunk query (filled for uncertified ones)
+    auto read_sk = [&](int cnt, const std::vector<int>& local, const std::vector<int>* map) -> int {
+      std::vector<uint64_t> skv((size_t)cnt);
+      HIPC(hipMemcpy(skv.data(), ix->w_sk.p, (size_t)cnt * 8, hipMemcpyDeviceToHost));
+      if (sk_chunk.empty()) sk_chunk.assign((size_t)m, 0ull);
+      for (int j : local) sk_chunk[(size_t)(map ? (*map)[j] : j)] = skv[(size_t)j];
+      return HCR_OK;
+    };
+    if (n_unc > 0) CHECK(read_sk(m, unc, nullptr));
     int kp = kp0;
     while (n_unc > 0 && kp < kMaxKprime) {
       kp = std::min(kMaxKprime, kp * 4);
@@ -894,6 +978,7 @@ static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k
         hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) rc = set_err(HCR_EHIP, "scatter: %s", hipGetErrorString(e));
       }
+      if (rc == HCR_OK && n2 > 0) rc = read_sk(nu, unc2, &unc);
       // map the still-uncertified subset back to chunk-local query indices
       std::vector<int> mapped;
       for (int j : unc2) mapped.push_back(unc[j]);
@@ -902,7 +987,14 @@ static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k
       unc.swap(mapped);
       n_unc = n2;
     }
-    ix->stats.uncertified_queries += n_unc;
+    if (n_unc > 0) {
+      // still uncertified at k' = 512 (clusters of near-ties wider than the candidate set, or
+      // an over-shot estimated seed): one exact fp64 scan per query group settles them
+      std::vector<uint64_t> sk((size_t)n_unc);
+      for (int j = 0; j < n_unc; ++j) sk[(size_t)j] = sk_chunk[(size_t)unc[j]];
+      CHECK(exact_fallback(ix, qc, unc, sk, k, mode, thr, os, oi, st));
+      ix->stats.fallback_queries += n_unc;
+    }
   }
   return HCR_OK;
 }
@@ -912,11 +1004,12 @@ extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t 
                                  int64_t* d_out_ids, void* stream) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
-  if (k <= 0 || k > 256) return set_err(HCR_EINVAL, "k must be in [1, 256], got %d", k);
+  if (k <= 0 || k > kMaxK) return set_err(HCR_EINVAL, "k must be in [1, %d], got %d", kMaxK, k);
   if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
     return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
   if (nq > 0 && (!d_queries || !d_out_scores || !d_out_ids)) return set_err(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
   // NULL = the legacy default stream (as every *_device entry point): the caller's work on
   // it (e.g. torch's default stream producing the input) is ordered before ours
   hipStream_t st = (hipStream_t)stream;
@@ -925,15 +1018,16 @@ extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t 
 }
 
 extern "C" int hcr_search(hcr_index* ix, const float* queries, int64_t nq, int k, int score_mode,
-                          float threshold, float* out_scores, int64_t* out_ids) {
+                          double threshold, double* out_scores, int64_t* out_ids) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
-  if (k <= 0 || k > 256) return set_err(HCR_EINVAL, "k must be in [1, 256], got %d", k);
+  if (k <= 0 || k > kMaxK) return set_err(HCR_EINVAL, "k must be in [1, %d], got %d", kMaxK, k);
   if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
     return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
   if (nq == 0) return HCR_OK;
   if (!queries || !out_scores || !out_ids) return set_err(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
   for (int64_t q0 = 0; q0 < nq; q0 += kQueryChunk) {
     const int64_t m = std::min<int64_t>(kQueryChunk, nq - q0);
     CHECK(ix->w_qin.ensure((size_t)m * ix->dim * 4));
@@ -941,12 +1035,10 @@ extern "C" int hcr_search(hcr_index* ix, const float* queries, int64_t nq, int k
     CHECK(ix->w_outi.ensure((size_t)m * k * 8));
     HIPC(hipMemcpyAsync(ix->w_qin.p, queries + q0 * ix->dim, (size_t)m * ix->dim * 4,
                         hipMemcpyHostToDevice, ix->stream));
-    CHECK(search_device_impl(ix, ix->w_qin.as<const float>(), m, k, score_mode, (double)threshold,
+    CHECK(search_device_impl(ix, ix->w_qin.as<const float>(), m, k, score_mode, threshold,
                              ix->w_outs.as<double>(), ix->w_outi.as<int64_t>(), ix->stream));
-    std::vector<double> s((size_t)m * k);
-    HIPC(hipMemcpy(s.data(), ix->w_outs.p, s.size() * 8, hipMemcpyDeviceToHost));
-    HIPC(hipMemcpy(out_ids + q0 * k, ix->w_outi.p, s.size() * 8, hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < s.size(); ++i) out_scores[q0 * k + i] = (float)s[i];
+    HIPC(hipMemcpy(out_scores + q0 * k, ix->w_outs.p, (size_t)m * k * 8, hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(out_ids + q0 * k, ix->w_outi.p, (size_t)m * k * 8, hipMemcpyDeviceToHost));
   }
   return HCR_OK;
 }
@@ -960,6 +1052,7 @@ extern "C" int hcr_score_all(hcr_index* ix, const float* queries, int64_t nq, in
   if (nq == 0 || ix->n == 0) return HCR_OK;
   if (!queries || !out_scores) return set_err(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
   const int64_t qc = 1024;
   for (int64_t q0 = 0; q0 < nq; q0 += qc) {
     const int m = (int)std::min<int64_t>(qc, nq - q0);

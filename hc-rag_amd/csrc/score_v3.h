@@ -26,16 +26,6 @@ namespace hcr {
 constexpr int V3_NIS = 3;   // tile slots of inverse norms / mask words / global bounds; the
                             // host requires (V3_NIS - 1) * ksteps > NST - 1
 
-#ifdef HCR_V3_STAMPS
-// diagnostic build only (tests/debug/v3_ablate.hip): per-wave cycle sums of the loop segments
-__device__ uint64_t* g_v3_stamps;
-#define V3_STAMP(t)                                                                  \
-  do {                                                                               \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");   \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-  } while (0)
-#endif
 
 template <int RT, int QT, int NST>
 struct V3Layout {
@@ -81,11 +71,7 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
-#ifndef HCR_V3_NO_QDMA
   const int my_pieces = (NP - wave + 7) / 8;               // DMA pieces this wave issues per stage
-#else
-  const int my_pieces = (NA - wave + 7) / 8;
-#endif
 
   // XCD-aware bijective remap: the query blocks sharing a partition run on one XCD
   const int nwg = gridDim.x, b = blockIdx.x;
@@ -129,11 +115,7 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   auto issue_stage = [&](int s_) {
     const int s = __builtin_amdgcn_readfirstlane(s_);
     const int vt = t0 + s / ksteps, ks = s - (s / ksteps) * ksteps;
-#ifdef HCR_V3_HOT_TILES
-    const int tile = (vt * tstride) % HCR_V3_HOT_TILES;   // diagnostic: L2-resident corpus
-#else
     const int tile = vt * tstride;
-#endif
     char* sa = lds + (s % NST) * L::STAGE;
     const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         uniform_ptr(rows_b + (size_t)tile * RT * ldb), (short)0, RT * ldb, 0x00020000);
@@ -142,9 +124,7 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     for (int i = 0; i < (NP + 7) / 8; ++i) {
       const int j = wave + 8 * i;                              // piece index (uniform)
       if (j < NA) dma16(a_rsrc, sa + j * 1024, voff, j * 16 * ldb + kofs);
-#ifndef HCR_V3_NO_QDMA
       else if (j < NP) dma16(q_rsrc, sa + L::A_BYTES + (j - NA) * 1024, voff, (j - NA) * 16 * ldb + kofs);
-#endif
     }
     if (ks == 0 && wave == 7)   // this tile's inverse norms (RT floats, 1 KiB piece)
       dma16(inv_rsrc, lds + L::INV + (vt % L::NIS) * L::INV_SLOT, lane * 16, tile * (RT * 4));
@@ -172,33 +152,13 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
 
   const int nsteps = (t1 - t0) * ksteps;
 
-#ifndef HCR_V3_NO_DMA
   for (int i = 0; i < D; ++i)
     if (i < nsteps) issue_stage(i);
-#endif
 
   int tile = t0, ks = 0;
   int ep_tile = -1;                      // tile whose epilogue is pending
-#ifdef HCR_V3_STAMPS
-  uint64_t st_epi = 0, st_wait = 0, st_issue = 0, st_mma = 0, ta, tb;
-#endif
   for (int s = 0; s <= nsteps; ++s) {
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(ta);
-#endif
     // 1) epilogue of the tile finished by step s-1 (accumulators complete)
-#ifdef HCR_V3_NO_EPI
-    if (ep_tile >= 0) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-          if (acc[m][n][0] == 12345.f) cnt[0] = 1;     // keep the accumulators alive
-          acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-      ep_tile = -1;
-    }
-#endif
     if (ep_tile >= 0) {
       int* prev_flag = flag + ((ep_tile + 1) & 1);
       if (v3_lds_u32(prev_flag)) {       // set >= 1 barrier ago; uniform across the block
@@ -288,9 +248,6 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       ep_tile = -1;
     }
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_epi += tb - ta; ta = tb;
-#endif
     if (s == nsteps) break;
 
     // 2) stage s landed: this wave's pieces (later stages may stay in flight), then everyone's
@@ -299,15 +256,7 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       v3_wait_vmcnt(later * my_pieces);
     }
     v3_barrier();                        // also: every wave is done reading stage s-1's slot
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_wait += tb - ta; ta = tb;
-#endif
-#ifndef HCR_V3_NO_DMA
     if (s + D < nsteps) issue_stage(s + D);
-#endif
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_issue += tb - ta; ta = tb;
-#endif
 
     // 3) MFMAs of stage s
     const bool last_k = (ks == ksteps - 1);
@@ -324,27 +273,14 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < NQ; ++n) {
-#ifndef HCR_V3_NO_MFMA
           acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-#else
-          acc[m][n][0] += (float)av[m][0] * (float)bq[n][0];
-#endif
         }
       __builtin_amdgcn_sched_group_barrier(0x100, NQ + MT, 0);   // DS reads
       __builtin_amdgcn_sched_group_barrier(0x008, MT * NQ, 0);   // MFMAs
     }
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_mma += tb - ta; ta = tb;
-#endif
     if (last_k) ep_tile = tile;
     if (++ks == ksteps) { ks = 0; ++tile; }
   }
-#ifdef HCR_V3_STAMPS
-  if (lane == 0 && g_v3_stamps) {
-    uint64_t* o = g_v3_stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
-    o[0] = st_epi; o[1] = st_wait; o[2] = st_issue; o[3] = st_mma;
-  }
-#endif
 
   // final: every query's best kp keys -> partials[q][p][0..kp).  All waves' appends first.
   __syncthreads();

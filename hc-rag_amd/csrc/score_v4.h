@@ -25,11 +25,6 @@ namespace hcr {
 
 constexpr int V4_RT = 256, V4_QT = 256;
 
-#ifdef HCR_V4_COUNT
-// diagnostic build only: [0] slow-path entries, [1] appends (per wave), [2] epilogues (per
-// wave), [3] in-loop compactions (per workgroup)
-__device__ unsigned long long g_v4_count[4];
-#endif
 
 template <int NST>
 struct V4Layout {
@@ -176,10 +171,8 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
       const int j = wave + 8 * i;
       dma16(d.a, d.sa + j * 1024, voff, j * 16 * ldb + d.kofs);
     } else {
-#ifndef HCR_V4_NO_QDMA     // ablation: the query half of every stage not refilled (timing only)
       const int j = wave + 8 * (i - 2);
       dma16(d.q, d.sa + L::A_BYTES + j * 1024, voff, j * 16 * ldb + d.kofs);
-#endif
     }
   };
   auto advance_cursor = [&]() {
@@ -215,48 +208,11 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   int rslot = 0;                         // ring slot of the stage being consumed
   int ks = 0, vt = t0;
   int ep_vt = -1;                        // virtual tile whose epilogue is pending
-#ifdef HCR_V3_STAMPS
-  uint64_t st_epi = 0, st_wait = 0, st_issue = 0, st_mma = 0, ta, tb;
-#endif
   for (int s = 0; s <= nsteps; ++s) {
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(ta);
-#endif
     // 1) epilogue of the tile finished by step s-1
-#ifdef HCR_V3_NO_EPI
-    if (ep_vt >= 0) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-          if (acc[m][n][0] == 12345.f) cnt[0] = 1;
-          acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-        }
-      ep_vt = -1;
-    }
-#endif
-#ifdef HCR_V4_EPI_READONLY
-    if (ep_vt >= 0) {               // ablation: tile values read + bound, no scan
-      const int slot = ep_vt % L::NIS;
-      const int lr = lane & 15, lq = lane >> 4;
-      V4TileVals tv;
-      v4_read_tile_vals(lds_addr(ring + L::INV + slot * 1024 + (wm * 128 + lq * 4) * 4),
-                        lds_addr(ring + L::TG + slot * 1024 + (wn * 64 + lr) * 4),
-                        lds_addr(ring + L::MSK + slot * 64 + wm * 16), tv);
-      if (tv.tg[0] == 12345u && tv.iv[3].x == 2.f) cnt[0] = 1;
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-      ep_vt = -1;
-    }
-#endif
     if (ep_vt >= 0) {
       int* prev_flag = flag + ((ep_vt + 1) & 1);
       if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
-#ifdef HCR_V4_COUNT
-        if (tid == 0) atomicAdd(&g_v4_count[3], 1ull);
-#endif
         __syncthreads();                 // other waves' candidate stores (global) are visible
         for (int ql = wave; ql < QT; ql += V3_NT / 64) {
           if (cnt[ql] > CAP - RT)
@@ -328,15 +284,7 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
           any |= hit[n];
         }
         if constexpr (MAXONLY) any = false;
-#ifdef HCR_V4_NO_SLOW
-        if (__any(any) && lane == 0) cnt[wave] += 1;   // ablation: fast path only
-        if (false) {
-#else
         if (__any(any)) {
-#endif
-#ifdef HCR_V4_COUNT
-          if (lane == 0) atomicAdd(&g_v4_count[0], 1ull);
-#endif
 #pragma unroll
           for (int n = 0; n < NQ; ++n) {
             if (hit[n]) {
@@ -350,9 +298,6 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
                     const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
                     const uint64_t key = make_key(sc, rowl);
                     if (key > tkr[n]) {
-#ifdef HCR_V4_COUNT
-                      atomicAdd(&g_v4_count[1], 1ull);
-#endif
                       const int pos = v3_lds_add_rtn(&cnt[ql], 1);
                       wbuf[(size_t)ql * CAP + pos] = key;
                       if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
@@ -363,9 +308,6 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
           }
         }
       };
-#ifdef HCR_V4_COUNT
-      if (lane == 0) atomicAdd(&g_v4_count[2], 1ull);
-#endif
       if (UNIT && !mask && row0 + RT <= n_rows) epi(std::true_type{});
       else epi(std::false_type{});
 #pragma unroll
@@ -374,21 +316,11 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       ep_vt = -1;
     }
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_epi += tb - ta; ta = tb;
-#endif
     if (s == nsteps) break;
 
     // 2) stage s landed (this wave's pieces; D-1 later stages stay in flight), then everyone's
-#ifdef HCR_V4_NO_QDMA
-    v3_wait_vmcnt((D - 1) * 2);
-#else
     v3_wait_vmcnt((D - 1) * 4);
-#endif
     v3_barrier();
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_wait += tb - ta; ta = tb;
-#endif
 
     // 3) tile-slot pieces for the stage being issued (once per tile), then the MFMAs of stage s
     //    with the 4 pieces of stage s + D between them
@@ -397,23 +329,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     {
       const char* st = ring + rslot * L::STAGE;
       V bq[NQ], av[MT];
-#ifdef HCR_V4_SPLITREAD
-      // fragments land in issue order; each MFMA group waits only for its own two row blocks
-      v4_issue_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
-#else
       v4_read_frags<V>(lds_addr(st + offA), lds_addr(st + offB), av, bq);
-#endif
-#ifdef HCR_V3_STAMPS
-      V3_STAMP(tb); st_issue += tb - ta; ta = tb;
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-#ifdef HCR_V4_SPLITREAD
-        if (i == 0) v4_frag_wait6<6>(av[0], av[1], bq);
-        if (i == 1) v4_frag_wait<4>(av[2], av[3]);
-        if (i == 2) v4_frag_wait<2>(av[4], av[5]);
-        if (i == 3) v4_frag_wait<0>(av[6], av[7]);
-#endif
 #pragma unroll
         for (int m = 2 * i; m < 2 * i + 2; ++m)
 #pragma unroll
@@ -426,21 +344,12 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);       // 1 DMA piece
       }
     }
-#ifdef HCR_V3_STAMPS
-    V3_STAMP(tb); st_mma += tb - ta; ta = tb;
-#endif
     advance_cursor();
     rslot = (rslot + 1 == NST) ? 0 : rslot + 1;
     if (ks == ksteps - 1) ep_vt = vt;
     if (++ks == ksteps) { ks = 0; ++vt; }
   }
 
-#ifdef HCR_V3_STAMPS
-  if (lane == 0 && g_v3_stamps) {
-    uint64_t* o = g_v3_stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
-    o[0] = st_epi; o[1] = st_wait; o[2] = st_issue; o[3] = st_mma;
-  }
-#endif
   if constexpr (MAXONLY) return;
   __syncthreads();
   for (int ql = wave; ql < QT; ql += V3_NT / 64) {

@@ -20,6 +20,13 @@ namespace hcr {
 
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
 
+// Global id of a shard-local row: the index's id map when rows were added with explicit ids
+// (hcr_index_add_ids), else id_offset + row.
+__device__ __forceinline__ int64_t row_id(int64_t id_offset, const int64_t* __restrict__ idmap,
+                                          uint32_t row) {
+  return idmap ? idmap[row] : id_offset + (int64_t)row;
+}
+
 // -------------------------------------------------------------------------------------
 // K0: ingest. One wave per row.
 // -------------------------------------------------------------------------------------
@@ -384,306 +391,6 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
 }
 
 // -------------------------------------------------------------------------------------
-// K2 v2 (large batches, 16-bit storage): 224 corpus rows x 256 queries per workgroup.
-//   8 waves = 2 (rows) x 4 (queries); wave tile 112 rows x 64 queries = 7 x 4 accumulators
-//   of MFMA 16x16x32 (119 flop per byte re-read from L2, vs 64 for the 128 x 128 tile).
-//   Operands are staged by LDS-DMA (buffer_load ... lds: no staging VGPRs); the XOR swizzle
-//   is applied to the per-lane SOURCE offset so the lane-linear LDS image matches the
-//   conflict-free fragment reads.  Two LDS stages: the DMA for stage s+1 is issued before
-//   the epilogue / MFMAs of stage s and retired by the barrier that ends stage s.  Per-tile
-//   inverse norms and row-mask words arrive the same way (3 rotating slots).
-//   224 rows (not 256) keeps the whole LDS image, and every DMA target, below 128 KiB.
-//   Requires: rows / inv_norm / mask allocated with >= 256 rows of slack past the last
-//   tile, qhat allocated to nqb*256 rows (padding rows zero).
-// -------------------------------------------------------------------------------------
-constexpr int R2 = 224, Q2 = 256, NT2 = 512;
-constexpr int MT2 = R2 / 32;                                    // m-tiles per wave (7)
-constexpr int A2_BYTES = R2 * BK * 2, B2_BYTES = Q2 * BK * 2;   // 28 KiB + 32 KiB
-constexpr int STAGE2 = A2_BYTES + B2_BYTES;
-constexpr int L2_INV = 2 * STAGE2;                              // 3 x 1 KiB inverse norms
-constexpr int L2_MSK = L2_INV + 3 * 1024;                       // 3 x 8 row-mask words
-constexpr int L2_TAU = L2_MSK + 3 * 64;                         // u64 tau_key[256]
-constexpr int L2_CNT = L2_TAU + Q2 * 8;                         // int cnt[256]
-constexpr int L2_FLAG = L2_CNT + Q2 * 4;                        // int flag[2] (tile parity)
-constexpr int L2_TOTAL = L2_FLAG + 16;
-static_assert(L2_TOTAL <= 128 * 1024, "v2 LDS image must stay below 128 KiB");
-
-// LDS reads the compiler does not see: hipcc would otherwise wait vmcnt(0) for the
-// in-flight LDS-DMA of the next stage before them (a conservative alias assumption).
-template <typename TM, int CAP>
-__global__ void __launch_bounds__(NT2, 2)
-score_topk224_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ksteps,
-                     const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
-                     const TM* __restrict__ qhat, int nqb, int P, int ntiles,
-                     uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int kp, float* __restrict__ dbg = nullptr) {
-  using Op = MfmaOp<TM>;
-  using V = typename Op::V;
-  __shared__ __attribute__((aligned(16))) char lds[L2_TOTAL];
-  uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L2_TAU);
-  int* cnt = reinterpret_cast<int*>(lds + L2_CNT);
-  int* flag = reinterpret_cast<int*>(lds + L2_FLAG);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-
-  const int nwg = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int qb = g % nqb, p = g / nqb;
-  const int t0 = (int)((int64_t)p * ntiles / P);
-  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
-  const int qbase = qb * Q2;
-  uint64_t* wbuf = buf + (size_t)b * Q2 * CAP;
-
-  for (int i = tid; i < Q2; i += NT2) { tau_key[i] = 0ull; cnt[i] = 0; }
-  if (tid == 0) { flag[0] = 0; flag[1] = 0; }
-
-  if (t0 >= t1) {
-    for (int i = tid; i < Q2 * kp; i += NT2) {
-      const int ql = i / kp, j = i - ql * kp;
-      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
-    }
-    return;
-  }
-
-  // LDS-DMA: one 32-bit voffset per lane (row inside an 8-row group + swizzled chunk); the
-  // group and K offsets go in the scalar soffset, the tile base in the descriptor.
-  const int lrow = lane >> 3;
-  const int ldb = ld * 2;                                      // row pitch in bytes
-  const int voff = lrow * ldb + (((lane & 7) ^ lrow) << 4);
-  const char* rows_b = reinterpret_cast<const char*>(rows);
-  const __amdgpu_buffer_rsrc_t q_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(reinterpret_cast<const char*>(qhat) + (size_t)qbase * ldb), (short)0, Q2 * ldb,
-      0x00020000);
-  const __amdgpu_buffer_rsrc_t inv_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(inv_norm), (short)0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t msk_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(mask), (short)0, 0x7FFFFFFF, 0x00020000);
-
-  auto issue_stage = [&](int tile_, int ks_, int stg_) {
-    const int tile = __builtin_amdgcn_readfirstlane(tile_);   // provably uniform descriptor
-    const int ks = __builtin_amdgcn_readfirstlane(ks_);       // inputs: no waterfall loops
-    const int stg = __builtin_amdgcn_readfirstlane(stg_);
-    char* sa = lds + stg * STAGE2;
-    const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(rows_b + (size_t)tile * R2 * ldb), (short)0, 256 * ldb, 0x00020000);
-    const int kofs = ks * (BK * 2);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int grp = wave * 4 + i;                            // 8-row group
-      const int so = grp * 8 * ldb + kofs;
-      if (grp < R2 / 8) dma16(a_rsrc, sa + grp * 1024, voff, so);
-      dma16(q_rsrc, sa + A2_BYTES + grp * 1024, voff, so);
-    }
-    if (ks == 0 && wave == 0)   // 256 floats (224 used) of this tile's inverse norms
-      dma16(inv_rsrc, lds + L2_INV + (tile % 3) * 1024, lane * 16, tile * (R2 * 4));
-    if (ks == 0 && wave == 1 && mask) {
-      if (lane < 8)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            msk_rsrc, (__attribute__((address_space(3))) void*)(lds + L2_MSK + (tile % 3) * 64),
-            4, lane * 4, tile * (R2 / 8), 0, 0);
-    }
-  };
-
-  // fragment read offsets
-  const int fr = lane & 15;
-  const int c0 = (lane >> 4) ^ (lane & 7);
-  const int offA0 = (wm * (R2 / 2) + fr) * 128 + (c0 << 4);
-  const int offA1 = (wm * (R2 / 2) + fr) * 128 + ((c0 ^ 4) << 4);
-  const int offB0 = A2_BYTES + (wn * 64 + fr) * 128 + (c0 << 4);
-  const int offB1 = A2_BYTES + (wn * 64 + fr) * 128 + ((c0 ^ 4) << 4);
-
-  floatx4 acc[MT2][4];
-#pragma unroll
-  for (int m = 0; m < MT2; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  uint32_t tg[4] = {0u, 0u, 0u, 0u};
-  const int nsteps = (t1 - t0) * ksteps;
-
-  issue_stage(t0, 0, 0);
-  __syncthreads();
-
-  int tile = t0, ks = 0;
-  int ep_tile = -1;                      // tile whose epilogue is pending
-  for (int s = 0; s <= nsteps; ++s) {
-    // 1) DMA of the next stage (its buffer was last read in step s-1, before its barrier)
-    int ntile = tile, nks = ks + 1;
-    if (nks == ksteps) { nks = 0; ++ntile; }
-    if (s + 1 < nsteps) issue_stage(ntile, nks, (s + 1) & 1);
-
-    // 2) epilogue of the tile finished by step s-1 (accumulators complete)
-    if (ep_tile >= 0) {
-      // flag[t & 1] is set by epilogue t and consumed (then cleared) at epilogue t + 1,
-      // so a clear never races with the sets of the epilogue that follows it.
-      int* prev_flag = flag + ((ep_tile + 1) & 1);
-      if (*prev_flag) {                  // set >= 1 barrier ago; uniform across the block
-        for (int ql = wave; ql < Q2; ql += NT2 / 64) {
-          if (cnt[ql] > CAP - R2)
-            compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
-                               tau_g + qbase + ql, kp, lane, nullptr);
-        }
-        __syncthreads();
-        if (tid == 0) *prev_flag = 0;
-      }
-      int* cur_flag = flag + (ep_tile & 1);
-      // per-lane addresses are derived from an opaque copy of the lane id so the compiler
-      // recomputes them here instead of hoisting them (and spilling) across the main loop
-      int le;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
-      const int lr = le & 15, lq = le >> 4;
-      const int64_t row0 = (int64_t)ep_tile * R2;
-      const char* invl = lds + L2_INV + (ep_tile % 3) * 1024;
-      const char* mskl = lds + L2_MSK + (ep_tile % 3) * 64;
-      float thr[4];
-      uint64_t tk[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int ql = wn * 64 + n * 16 + lr;
-        tk[n] = tau_key[ql];
-        const float ls = tk[n] ? key_score(tk[n]) : -INFINITY;
-        thr[n] = fmaxf(ls, unord32(tg[n]));
-      }
-      // inverse norm (NaN for rows past the end / masked out) of this lane's rows in m-tile m
-      auto inv4 = [&](int m, float (&iv)[4]) {
-        const int rl = wm * (R2 / 2) + m * 16 + lq * 4;        // row inside the tile
-        const float4 v = lds_read_f4_now(invl + rl * 4);
-        uint32_t mword = 0xFFFFFFFFu;
-        if (mask) mword = lds_read_u32_now(mskl + (rl >> 5) * 4);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (row0 + rl + r < n_rows) && ((mword >> ((rl + r) & 31)) & 1u);
-          iv[r] = ok ? vv[r] : __builtin_nanf("");
-        }
-      };
-      float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-      for (int m = 0; m < MT2; ++m) {
-        float iv[4];
-        inv4(m, iv);
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r] * iv[r]);
-      }
-      bool hit[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) hit[n] = mx[n] >= thr[n];
-#ifndef HCR_DBG_FINAL_RECORD
-      if (dbg) {                          // debug harness only: coarse scores [q][row]
-        for (int m = 0; m < MT2; ++m) {
-          float iv[4];
-          inv4(m, iv);
-          for (int n = 0; n < 4; ++n)
-            for (int r = 0; r < 4; ++r) {
-              const int64_t row = row0 + wm * (R2 / 2) + m * 16 + lq * 4 + r;
-              if (row < n_rows)
-                dbg[(size_t)(qbase + wn * 64 + n * 16 + lr) * n_rows + row] = acc[m][n][r] * iv[r];
-            }
-        }
-      }
-#endif
-#ifndef HCR_DBG_NO_APPEND
-      if (__any(hit[0] | hit[1] | hit[2] | hit[3])) {
-#pragma unroll
-        for (int m = 0; m < MT2; ++m) {
-          float iv[4];
-          inv4(m, iv);
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            if (hit[n]) {
-              const int ql = wn * 64 + n * 16 + lr;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float sc = acc[m][n][r] * iv[r];
-                if (sc >= thr[n]) {
-                  const uint32_t rowl = (uint32_t)(row0 + wm * (R2 / 2) + m * 16 + lq * 4 + r);
-                  const uint64_t key = make_key(sc, rowl);
-                  if (key > tk[n]) {
-                    const int pos = atomicAdd(&cnt[ql], 1);
-                    wbuf[(size_t)ql * CAP + pos] = key;
-                    if (pos + 1 > CAP - R2) *cur_flag = 1;
-                  }
-                }
-              }
-            }
-          }
-        }
-      }
-#endif
-#pragma unroll
-      for (int m = 0; m < MT2; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-      ep_tile = -1;
-    }
-    if (s == nsteps) break;
-
-    // 3) MFMAs of step s
-    const bool last_k = (ks == ksteps - 1);
-#ifndef HCR_DBG_NO_TG
-    if (last_k) {
-      int lt;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(lt) : "v"(lane));
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-        tg[n] = __hip_atomic_load(tau_g + qbase + wn * 64 + n * 16 + (lt & 15), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
-    {
-      const char* st = lds + (s & 1) * STAGE2;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int oa = kk ? offA1 : offA0;
-        const int ob = kk ? offB1 : offB0;
-        V bq[4];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bq[n] = *reinterpret_cast<const V*>(st + ob + n * 16 * 128);
-#pragma unroll
-        for (int m = 0; m < MT2; ++m) {
-          const V av = *reinterpret_cast<const V*>(st + oa + m * 16 * 128);
-#pragma unroll
-          for (int n = 0; n < 4; ++n) acc[m][n] = Op::run(av, bq[n], acc[m][n]);
-        }
-      }
-    }
-    __syncthreads();                     // retires the DMA of stage s+1 (vmcnt(0) + barrier)
-    if (last_k) ep_tile = tile;
-    tile = ntile;
-    ks = nks;
-  }
-
-  // final: every query's best kp keys -> partials[q][p][0..kp).  Both row halves (wm) of
-  // the last epilogue append to the same queries: wait for all of them.
-  __syncthreads();
-#ifdef HCR_DBG_FINAL_RECORD
-  {
-    uint64_t* rec = reinterpret_cast<uint64_t*>(dbg);
-    for (int ql = wave; ql < Q2; ql += NT2 / 64) {
-      uint64_t* o = partials + ((size_t)(qbase + ql) * P + p) * kp;
-      const int c = cnt[ql];
-      if (lane == 0) {
-        rec[((size_t)(qbase + ql) * P + p) * 4 + 0] = (uint64_t)(uintptr_t)o;
-        rec[((size_t)(qbase + ql) * P + p) * 4 + 1] = (uint64_t)c;
-        rec[((size_t)(qbase + ql) * P + p) * 4 + 2] = (uint64_t)(uintptr_t)(wbuf + (size_t)ql * CAP);
-        rec[((size_t)(qbase + ql) * P + p) * 4 + 3] = (uint64_t)(uintptr_t)(tau_g + qbase + ql);
-      }
-    }
-  }
-#elif !defined(HCR_DBG_NO_FINAL)
-  for (int ql = wave; ql < Q2; ql += NT2 / 64) {
-    compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
-                       lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
-  }
-#endif
-}
-
-// -------------------------------------------------------------------------------------
 // K3: merge the P partition lists of one query into its global top-k' (sorted desc).
 // -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
@@ -736,7 +443,8 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
                const TS* __restrict__ rows, int ld, const double* __restrict__ norm64, int k,
                int mode, double thr, int64_t id_offset, double* __restrict__ out_s,
                int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
-               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est = nullptr) {
+               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
+               uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap) {
   extern __shared__ __attribute__((aligned(16))) char sm_raw[];
   double* qd = reinterpret_cast<double*>(sm_raw);
   uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
@@ -809,6 +517,9 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
     }
     unc_flags[q] = cert ? 0 : 1;
     if (!cert) atomicAdd(unc_count, 1);
+    // s_k of the candidates (a lower bound on the true k-th best exact score): the starting
+    // threshold of the exact fallback for queries that stay uncertified
+    if (sk_out) sk_out[q] = nvalid >= k ? hi[k - 1] : 0ull;
   }
   for (int t = threadIdx.x; t < k; t += blockDim.x) {
     double s = -INFINITY;
@@ -816,11 +527,108 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
     if (t < nvalid) {
       double v = unord64(hi[t]);
       if (mode == 1) v = (v + 1.0) / 2.0;
-      if (v >= thr) { s = v; id = id_offset + (int64_t)(0xFFFFFFFFu - (uint32_t)lo[t]); }
+      if (v >= thr) { s = v; id = row_id(id_offset, idmap, 0xFFFFFFFFu - (uint32_t)lo[t]); }
     }
     out_s[(size_t)q * k + t] = s;
     out_i[(size_t)q * k + t] = id;
   }
+}
+
+// -------------------------------------------------------------------------------------
+// K6/K7: exact fallback (queries the certificate could not settle at k' = 512, and k > 256).
+//   K6 scans every row once for a group of queries: fp64 cosine in the same summation order
+//   as K4 (so the scores are bit-identical), and appends each row whose key (score desc, row
+//   asc) is >= the query's threshold key to a per-query buffer of `cap` slots.
+//   K7 sorts a query's buffer in LDS.  If it did not overflow it holds every row at or above
+//   the threshold, which is <= the true k-th best key, so its top-k IS the exact top-k.  If it
+//   overflowed, the k-th best of the slots it kept is a tighter threshold (still <= the true
+//   k-th best, and strictly above the old one because cap > k and keys are unique): the host
+//   re-runs K6 for those queries.  Starting threshold: K4's s_k (the k-th best exact score
+//   among the candidates), or the lowest key.
+// -------------------------------------------------------------------------------------
+template <typename TS>
+__global__ void __launch_bounds__(256)
+exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
+                    const double* __restrict__ qnorm, const TS* __restrict__ rows, int ld,
+                    int64_t n, const double* __restrict__ norm64,
+                    const uint32_t* __restrict__ maskbits, const uint64_t* __restrict__ th_hi,
+                    const uint64_t* __restrict__ th_lo, const int* __restrict__ active, int cap,
+                    unsigned int* __restrict__ cnt, uint64_t* __restrict__ buf_hi,
+                    uint64_t* __restrict__ buf_lo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t row = w0; row < n; row += nw) {
+    if (maskbits && !((maskbits[row >> 5] >> (row & 31)) & 1u)) continue;
+    const TS* e = rows + row * ld;
+    const double nr = norm64[row];
+    for (int q = 0; q < nq; ++q) {
+      if (!active[q]) continue;
+      const float* qs = q32 + (int64_t)q * dim;
+      double acc = 0.0;
+      for (int d = lane; d < dim; d += 64) acc += (double)qs[d] * (double)(float)e[d];
+      acc = wave_sum_f64(acc);
+      if (lane == 0) {
+        const uint64_t h = ord64(acc / (qnorm[q] * nr));
+        const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)row);
+        if (h > th_hi[q] || (h == th_hi[q] && l >= th_lo[q])) {
+          const unsigned int p = atomicAdd(&cnt[q], 1u);
+          if (p < (unsigned int)cap) {
+            buf_hi[(size_t)q * cap + p] = h;
+            buf_lo[(size_t)q * cap + p] = l;
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
+                    const uint64_t* __restrict__ buf_hi, const uint64_t* __restrict__ buf_lo,
+                    uint64_t* __restrict__ th_hi, uint64_t* __restrict__ th_lo,
+                    int* __restrict__ active, int* __restrict__ n_again, int mode, double thr,
+                    int64_t id_offset, const int64_t* __restrict__ idmap,
+                    const int* __restrict__ out_idx, double* __restrict__ out_s,
+                    int64_t* __restrict__ out_i) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm_sel[];
+  const int q = blockIdx.x;
+  if (!active[q]) return;
+  const unsigned int c = cnt[q];
+  const int nload = (int)min(c, (unsigned int)cap);
+  int m = 1;
+  while (m < nload || m < k) m <<= 1;                  // <= cap (power of two, cap > k)
+  uint64_t* hi = sm_sel;
+  uint64_t* lo = sm_sel + m;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    const bool v = i < nload;
+    hi[i] = v ? buf_hi[(size_t)q * cap + i] : 0ull;
+    lo[i] = v ? buf_lo[(size_t)q * cap + i] : 0ull;
+  }
+  __syncthreads();
+  block_sort_desc_pair(hi, lo, m);
+  if (c > (unsigned int)cap) {
+    if (threadIdx.x == 0) {
+      th_hi[q] = hi[k - 1];
+      th_lo[q] = lo[k - 1];
+      atomicAdd(n_again, 1);
+    }
+    return;
+  }
+  const int o = out_idx[q];
+  for (int t = threadIdx.x; t < k; t += blockDim.x) {
+    double s = -INFINITY;
+    int64_t id = -1;
+    if (t < nload) {
+      double v = unord64(hi[t]);
+      if (mode == 1) v = (v + 1.0) / 2.0;
+      if (v >= thr) { s = v; id = row_id(id_offset, idmap, 0xFFFFFFFFu - (uint32_t)lo[t]); }
+    }
+    out_s[(size_t)o * k + t] = s;
+    out_i[(size_t)o * k + t] = id;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) active[q] = 0;
 }
 
 // -------------------------------------------------------------------------------------
@@ -897,6 +705,10 @@ __global__ void scatter_topk(const double* __restrict__ s, const int64_t* __rest
     out_s[(int64_t)idx[i] * k + j] = s[(int64_t)i * k + j];
     out_i[(int64_t)idx[i] * k + j] = ids[(int64_t)i * k + j];
   }
+}
+__global__ void iota_ids_kernel(int64_t* __restrict__ ids, int64_t n, int64_t first) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ids[i] = first + i;
 }
 __global__ void fill_empty(double* __restrict__ s, int64_t* __restrict__ ids, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -28,7 +28,8 @@ class SearchStats(ctypes.Structure):
     _fields_ = [("kprime", c_int32), ("widened_queries", c_int32),
                 ("uncertified_queries", c_int32), ("partitions", c_int32),
                 ("score_launches", c_int32), ("workgroups", c_int32),
-                ("score_kernel_ms", c_double), ("unit_kernel", c_int32)]
+                ("score_kernel_ms", c_double), ("unit_kernel", c_int32),
+                ("fallback_queries", c_int32), ("fallback_rounds", c_int32)]
 
 
 class BertConfig(ctypes.Structure):
@@ -50,13 +51,14 @@ _SIGS = {
     "hcr_index_add": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
     "hcr_index_add_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "hcr_index_set_id_offset": (c_int, [c_void_p, c_int64]),
+    "hcr_index_add_ids": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p]),
     "hcr_index_size": (c_int64, [c_void_p]),
     "hcr_index_dim": (c_int, [c_void_p]),
     "hcr_index_dtype": (c_int, [c_void_p]),
     "hcr_index_get_rows": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_float)]),
     "hcr_index_set_rowmask": (c_int, [c_void_p, POINTER(c_uint8), c_int64]),
-    "hcr_search": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, c_int, c_float,
-                           POINTER(c_float), POINTER(c_int64)]),
+    "hcr_search": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, c_int, c_double,
+                           POINTER(c_double), POINTER(c_int64)]),
     "hcr_search_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_double,
                                   c_void_p, c_void_p, c_void_p]),
     "hcr_score_all": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, POINTER(c_double)]),
@@ -64,6 +66,17 @@ _SIGS = {
     "hcr_index_set_timing": (c_int, [c_void_p, c_int]),
     "hcr_merge_topk_device": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
                                       c_void_p, c_void_p]),
+    "hcr_multi_create": (c_int, [c_int, POINTER(c_int), c_int, c_int, c_int64, POINTER(c_void_p)]),
+    "hcr_multi_destroy": (c_int, [c_void_p]),
+    "hcr_multi_add": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
+    "hcr_multi_set_rowmask": (c_int, [c_void_p, POINTER(c_uint8), c_int64]),
+    "hcr_multi_search": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, c_int, c_double,
+                                 POINTER(c_double), POINTER(c_int64)]),
+    "hcr_multi_size": (c_int64, [c_void_p]),
+    "hcr_multi_num_shards": (c_int, [c_void_p]),
+    "hcr_multi_shard_size": (c_int64, [c_void_p, c_int]),
+    "hcr_multi_exchange_kind": (c_int, [c_void_p]),
+    "hcr_multi_last_stats": (c_int, [c_void_p, POINTER(SearchStats)]),
     "hcr_wordpiece_create": (c_int, [c_char_p, c_int, c_int, POINTER(c_void_p)]),
     "hcr_wordpiece_create_from_buffer": (c_int, [c_char_p, c_int64, c_int, c_int,
                                                  POINTER(c_void_p)]),
@@ -73,6 +86,7 @@ _SIGS = {
                              POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
     "hcr_encoder_create": (c_int, [c_int, POINTER(BertConfig), c_int, POINTER(c_void_p)]),
     "hcr_encoder_destroy": (c_int, [c_void_p]),
+    "hcr_encoder_compute_dtype": (c_int, [c_void_p]),
     "hcr_encoder_set_weight": (c_int, [c_void_p, c_char_p, c_void_p, c_int64]),
     "hcr_encoder_finalize": (c_int, [c_void_p]),
     "hcr_encode": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
@@ -118,6 +132,14 @@ def _bind_hip_runtime():
         p = os.path.join(tl, name)
         if os.path.exists(p):
             ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    # torch's RCCL (SONAME librccl.so.1): the multi-device index dlopens that SONAME, so the
+    # process keeps one RCCL on one HIP runtime
+    p = os.path.join(tl, "librccl.so")
+    if os.path.exists(p):
+        try:
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        except OSError:
+            pass
     _runtime = hip
 
 

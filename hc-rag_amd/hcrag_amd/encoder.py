@@ -29,8 +29,12 @@ import numpy as np
 from ._lib import BertConfig, check, lib
 from .tokenizer import WordPieceTokenizer
 
-HCR_F16, HCR_BF16 = 0, 1
-_DTYPES = {"f16": HCR_F16, "fp16": HCR_F16, "float16": HCR_F16,
+HCR_F16, HCR_BF16, HCR_F32 = 0, 1, 2
+# "f32": reference precision (split-f16 MFMA GEMMs, fp32 attention / LayerNorm; the reference
+# encodes in fp32 torch, experiments/embedding_generator.py:124) -- the default.
+# "f16" / "bf16": fast modes (16-bit MFMA operands, fp32 accumulation).
+_DTYPES = {"f32": HCR_F32, "fp32": HCR_F32, "float32": HCR_F32,
+           "f16": HCR_F16, "fp16": HCR_F16, "float16": HCR_F16,
            "bf16": HCR_BF16, "bfloat16": HCR_BF16}
 
 # all-MiniLM-L6-v2 (the reference's model, experiments/embedding_generator.py:21)
@@ -62,7 +66,9 @@ class BertEncoder:
     with any prefix (``bert.``, ``0.auto_model.``).
     """
 
-    def __init__(self, config: Mapping, state_dict: Mapping, dtype: str = "f16", device: int = 0):
+    def __init__(self, config: Mapping, state_dict: Mapping, dtype: str = "f32", device: int = 0):
+        if dtype not in _DTYPES:
+            raise ValueError(f"unknown encoder dtype {dtype!r} (f32 | f16 | bf16)")
         self.config = dict(config)
         self.hidden = int(self.config["hidden"])
         self.max_position = int(self.config["max_position"])
@@ -147,7 +153,7 @@ class SentenceEmbedder:
         self.batch_size = int(batch_size)
 
     @classmethod
-    def from_pretrained(cls, path: str, dtype: str = "f16", device: int = 0,
+    def from_pretrained(cls, path: str, dtype: str = "f32", device: int = 0,
                         max_seq_length: Optional[int] = None, batch_size: int = 32,
                         pooling: str = "mean", normalize: bool = True) -> "SentenceEmbedder":
         """Local sentence-transformers / HF snapshot directory (no download)."""
@@ -214,7 +220,7 @@ class MI355XEmbedding(SentenceEmbedder):
     ``embed_batch_size`` (llama-index default 10), embeddings always L2-normalised
     (``normalize_embeddings=True``), optional query / text instruction prefixes (bge-*-en)."""
 
-    def __init__(self, model_name: str, embed_batch_size: int = 10, dtype: str = "f16",
+    def __init__(self, model_name: str, embed_batch_size: int = 10, dtype: str = "f32",
                  device: int = 0, max_length: Optional[int] = None,
                  query_instruction: Optional[str] = None, text_instruction: Optional[str] = None,
                  pooling: str = "mean"):
@@ -248,3 +254,11 @@ class MI355XEmbedding(SentenceEmbedder):
     def get_text_embedding_batch(self, texts: Sequence[str], show_progress: bool = False,
                                  **_) -> List[List[float]]:
         return self._get_text_embeddings(list(texts))
+
+    def get_agg_embedding_from_queries(self, queries: Sequence[str], agg_fn=None) -> List[float]:
+        """llama-index BaseEmbedding semantics: each query through get_query_embedding (query
+        instruction applied), then the mean (or ``agg_fn``)."""
+        embs = [self._get_query_embedding(q) for q in queries]
+        if agg_fn is not None:
+            return agg_fn(embs)
+        return np.mean(np.asarray(embs), axis=0).tolist()

@@ -87,6 +87,19 @@ class VectorIndex:
         check(lib().hcr_index_add(self._h, a.ctypes.data_as(c_void_p), int(a.shape[0]), dt,
                                   1 if normalize else 0))
 
+    def add_ids(self, rows, ids, normalize: bool = True) -> None:
+        """Append rows with explicit global ids (searches report these ids)."""
+        a, dt = _np_rows(rows)
+        if a.ndim == 1:
+            a = a.reshape(1, -1)
+        ids = np.ascontiguousarray(np.asarray(ids, dtype=np.int64).reshape(-1))
+        if a.ndim != 2 or a.shape[1] != self.dim or ids.shape[0] != a.shape[0]:
+            raise ValueError(f"rows must be (n, {self.dim}) with n ids")
+        if a.shape[0] == 0:
+            return
+        check(lib().hcr_index_add_ids(self._h, a.ctypes.data_as(c_void_p), int(a.shape[0]), dt,
+                                      1 if normalize else 0, ids.ctypes.data_as(c_void_p)))
+
     def add_device(self, ptr: int, n: int, rows_dtype: int, normalize: bool = False,
                    stream: int = 0) -> None:
         """Append n rows already in HBM (device pointer, e.g. ``tensor.data_ptr()``)."""
@@ -122,18 +135,19 @@ class VectorIndex:
     # -- queries ------------------------------------------------------------------------
     def search(self, queries, k: int, score_mode: int = HCR_SCORE_COSINE,
                threshold: float = -np.inf):
-        """Top-k per query.  Returns (scores float32 [nq,k], ids int64 [nq,k]); -1 = empty."""
+        """Exact top-k per query (1 <= k <= 2048).  Returns (scores float64 [nq,k] -- the exact
+        fp64 cosine, mapped by ``score_mode`` --, ids int64 [nq,k]); -1 = empty slot."""
         q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))
         if q.shape[1] != self.dim:
             raise ValueError(
                 f"Incompatible dimension for X and Y matrices: X.shape[1] == {q.shape[1]} "
                 f"while Y.shape[1] == {self.dim}")
         nq = q.shape[0]
-        s = np.empty((nq, k), dtype=np.float32)
+        s = np.empty((nq, k), dtype=np.float64)
         i = np.empty((nq, k), dtype=np.int64)
         check(lib().hcr_search(self._h, q.ctypes.data_as(POINTER(c_float)), nq, int(k),
                                int(score_mode), float(threshold),
-                               s.ctypes.data_as(POINTER(c_float)),
+                               s.ctypes.data_as(POINTER(c_double)),
                                i.ctypes.data_as(POINTER(c_int64))))
         return s, i
 
@@ -165,6 +179,96 @@ class VectorIndex:
         check(lib().hcr_index_set_timing(self._h, 1 if enable else 0))
 
 
+class MultiDeviceIndex:
+    """One process, several GPUs (``hcr_multi_*``): rows sharded in
+    contiguous blocks over ``devices`` (a device may repeat), every shard searched concurrently,
+    per-shard exact top-k lists exchanged to ``devices[0]`` (RCCL all-gather over distinct
+    devices, peer copies otherwise) and merged there.  Same ``add`` / ``search`` /
+    ``set_rowmask`` surface and results as ``VectorIndex`` over all rows."""
+
+    def __init__(self, dim: int, devices, dtype: str = "f16", capacity: int = 0):
+        if dtype not in _DTYPES:
+            raise ValueError(f"unknown dtype {dtype!r}")
+        devs = [int(d) for d in devices]
+        if not devs:
+            raise ValueError("need at least one device")
+        arr = (ctypes.c_int * len(devs))(*devs)
+        self._h = c_void_p()
+        check(lib().hcr_multi_create(len(devs), arr, int(dim), _DTYPES[dtype], int(capacity),
+                                     ctypes.byref(self._h)))
+        self.dim = int(dim)
+        self.dtype = dtype
+        self.devices = devs
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().hcr_multi_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __len__(self) -> int:
+        return int(lib().hcr_multi_size(self._h))
+
+    def shard_sizes(self):
+        return [int(lib().hcr_multi_shard_size(self._h, j)) for j in range(len(self.devices))]
+
+    @property
+    def exchange(self) -> str:
+        """How the last search moved the per-shard lists: "rccl" or "peer"."""
+        return {1: "rccl", 0: "peer"}.get(int(lib().hcr_multi_exchange_kind(self._h)), "?")
+
+    def add(self, rows, normalize: bool = True) -> None:
+        a, dt = _np_rows(rows)
+        if a.ndim == 1:
+            a = a.reshape(1, -1)
+        if a.ndim != 2 or a.shape[1] != self.dim:
+            raise ValueError(f"rows must be (n, {self.dim}), got {a.shape}")
+        if a.shape[0] == 0:
+            return
+        check(lib().hcr_multi_add(self._h, a.ctypes.data_as(c_void_p), int(a.shape[0]), dt,
+                                  1 if normalize else 0))
+
+    def set_rowmask(self, mask) -> None:
+        if mask is None:
+            check(lib().hcr_multi_set_rowmask(self._h, None, 0))
+            return
+        m = np.ascontiguousarray(np.asarray(mask, dtype=bool).astype(np.uint8))
+        check(lib().hcr_multi_set_rowmask(self._h, m.ctypes.data_as(POINTER(c_uint8)),
+                                          int(m.shape[0])))
+
+    def search(self, queries, k: int, score_mode: int = HCR_SCORE_COSINE,
+               threshold: float = -np.inf):
+        q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))
+        if q.shape[1] != self.dim:
+            raise ValueError(
+                f"Incompatible dimension for X and Y matrices: X.shape[1] == {q.shape[1]} "
+                f"while Y.shape[1] == {self.dim}")
+        nq = q.shape[0]
+        s = np.empty((nq, k), dtype=np.float64)
+        i = np.empty((nq, k), dtype=np.int64)
+        check(lib().hcr_multi_search(self._h, q.ctypes.data_as(POINTER(c_float)), nq, int(k),
+                                     int(score_mode), float(threshold),
+                                     s.ctypes.data_as(POINTER(c_double)),
+                                     i.ctypes.data_as(POINTER(c_int64))))
+        return s, i
+
+    def last_stats(self) -> dict:
+        st = SearchStats()
+        check(lib().hcr_multi_last_stats(self._h, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in SearchStats._fields_}
+
+
 def merge_topk_device(scores_ptr: int, ids_ptr: int, g: int, nq: int, k: int,
                       out_scores_ptr: int, out_ids_ptr: int, stream: int = 0) -> None:
     """Merge g shards' [g][nq][k] exact top-k lists on device."""
@@ -173,5 +277,5 @@ def merge_topk_device(scores_ptr: int, ids_ptr: int, g: int, nq: int, k: int,
                                       c_void_p(stream or None)))
 
 
-__all__ = ["VectorIndex", "merge_topk_device", "HCR_SCORE_COSINE", "HCR_SCORE_UNIT",
+__all__ = ["VectorIndex", "MultiDeviceIndex", "merge_topk_device", "HCR_SCORE_COSINE", "HCR_SCORE_UNIT",
            "HCR_F16", "HCR_BF16", "HCR_F32", "_lib"]

@@ -30,7 +30,7 @@ typedef enum {
   HCR_OK = 0,
   HCR_EINVAL = -1,   /* invalid argument (the reference raises ValueError here) */
   HCR_EHIP = -2,     /* HIP runtime error */
-  HCR_ERCCL = -3,    /* collective error (reserved; collectives live in the Python host) */
+  HCR_ERCCL = -3,    /* RCCL error (multi-device index exchange) */
   HCR_ENOMEM = -4,   /* device allocation failed */
   HCR_EIO = -5       /* file / format error (encoder weights, vocab) */
 } hcr_status;
@@ -80,6 +80,11 @@ int hcr_index_add_device(hcr_index* index, const void* d_rows, int64_t n, int ro
 /* Global id of this index's row 0 (row-sharded indexes: shard offset).  Search results
  * report id_offset + local row. */
 int hcr_index_set_id_offset(hcr_index* index, int64_t id_offset);
+/* hcr_index_add with an explicit global id per row (host int64[n]); searches report these
+ * ids for the appended rows (earlier rows keep id_offset + row).  Used by the multi-device
+ * index's shards and by stores whose ids are not insertion order. */
+int hcr_index_add_ids(hcr_index* index, const void* rows, int64_t n, int rows_dtype,
+                      int normalize, const int64_t* ids);
 
 int64_t hcr_index_size(const hcr_index* index);
 int hcr_index_dim(const hcr_index* index);
@@ -89,18 +94,21 @@ int hcr_index_dtype(const hcr_index* index);
 int hcr_index_get_rows(const hcr_index* index, int64_t row0, int64_t n, float* out_rows);
 
 /* Restrict searches to rows whose mask byte is non-zero (NULL clears the mask).  `n` must
- * equal the index size.  Replaces the category filter of experiments/main.py:872-885. */
+ * equal the index size; rows appended later are visible until the mask is set again.
+ * Replaces the category filter of experiments/main.py:872-885. */
 int hcr_index_set_rowmask(hcr_index* index, const uint8_t* mask, int64_t n);
 
 /* Batched top-k search: for each of `nq` float32 queries, the k rows of best cosine
  * (sklearn semantics in fp64 on the stored values; tie rule score desc, id asc), mapped
- * by `score_mode`, then kept only if score >= `threshold` (pass -INFINITY for none).
- * Outputs (host, nq x k): scores (float32), ids (int64, -1 = empty slot, score -inf).
+ * by `score_mode`, then kept only if score >= `threshold` (fp64; pass -INFINITY for none).
+ * Outputs (host, nq x k): scores (float64, the exact fp64 cosine), ids (int64, -1 = empty
+ * slot, score -inf).  Always the exact top-k: certified candidates (k <= 256) or, for the
+ * queries the certificate cannot settle and for k > 256, an exact fp64 scan of every row.
  * Replaces cosine_similarity + np.argsort(...)[::-1][:top_k] + threshold filter of
  * experiments/main.py:841-849 (and :886-889), and get_top_k_embeddings behind
- * VectorContextRetriever (query_interface.py:200-204).  k <= 256. */
+ * VectorContextRetriever (query_interface.py:200-204).  1 <= k <= 2048. */
 int hcr_search(hcr_index* index, const float* queries, int64_t nq, int k, int score_mode,
-               float threshold, float* out_scores, int64_t* out_ids);
+               double threshold, double* out_scores, int64_t* out_ids);
 
 /* Device variant: queries (float32, nq x dim), outputs in device memory; fp64 scores so
  * that row-sharded results merge exactly across GPUs.  Kernels run on `stream` (NULL = the
@@ -118,7 +126,8 @@ int hcr_score_all(hcr_index* index, const float* queries, int64_t nq, int score_
                   double* out_scores);
 
 /* Statistics of the last search on this handle: candidates kept per query (k'), queries
- * whose top-k needed a widened candidate set, queries left uncertified after widening. */
+ * whose top-k needed a widened candidate set, queries returned uncertified (always 0: the
+ * exact fallback settles them), queries answered by the exact fallback scan and its rounds. */
 typedef struct {
   int32_t kprime;
   int32_t widened_queries;
@@ -129,6 +138,8 @@ typedef struct {
   double score_kernel_ms;     /* summed HIP-event time of those launches */
   int32_t unit_kernel;        /* 1: the UNIT score kernel ran (L2-normalised corpus, raw dot
                                  product as coarse score, widened certificate bound) */
+  int32_t fallback_queries;   /* queries answered by the exact fp64 scan (K6/K7) */
+  int32_t fallback_rounds;    /* K6/K7 rounds run (threshold tightenings + 1 per group) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
@@ -140,6 +151,32 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  * SURVEY.md §8(e).  Asynchronous on `stream`. */
 int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, int64_t nq,
                           int k, double* d_out_scores, int64_t* d_out_ids, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Single-process multi-device index (one process drives all g devices).
+ * Rows are sharded in contiguous blocks over `n_dev` devices (dev_ids may repeat: several
+ * shards on one GPU); each hcr_multi_add splits its rows into n_dev blocks, ids stay insertion
+ * order.  hcr_multi_search runs every shard's exact top-k concurrently (one host thread and
+ * stream per shard), exchanges the per-shard lists to dev_ids[0] -- RCCL all-gather over the
+ * distinct devices (ncclCommInitAll), or peer copies when devices repeat or RCCL is absent --
+ * and merges them there (K5).  Same results as one hcr_index over all rows.  Replaces the
+ * single matrix of experiments/main.py:762 / the vector store behind
+ * query_interface.py:200-204 when the corpus spans the GPUs of a node.
+ * ------------------------------------------------------------------------------------- */
+typedef struct hcr_multi_index hcr_multi_index;
+int hcr_multi_create(int n_dev, const int* dev_ids, int dim, int dtype, int64_t capacity_rows,
+                     hcr_multi_index** out);
+int hcr_multi_destroy(hcr_multi_index* m);
+int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, int rows_dtype, int normalize);
+int hcr_multi_set_rowmask(hcr_multi_index* m, const uint8_t* mask, int64_t n);
+int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_t nq, int k, int score_mode,
+                     double threshold, double* out_scores, int64_t* out_ids);
+int64_t hcr_multi_size(const hcr_multi_index* m);
+int hcr_multi_num_shards(const hcr_multi_index* m);
+int64_t hcr_multi_shard_size(const hcr_multi_index* m, int shard);
+/* 1: the last search exchanged lists by RCCL all-gather, 0: by peer copies. */
+int hcr_multi_exchange_kind(const hcr_multi_index* m);
+int hcr_multi_last_stats(const hcr_multi_index* m, hcr_search_stats* out);
 
 /* ---------------------------------------------------------------------------------------
  * WordPiece tokenizer (host).  Replaces HF tokenizers 0.21.1 (Rust) BertNormalizer +
@@ -179,10 +216,16 @@ typedef struct {
   int32_t normalize;       /* 1 = L2-normalise the pooled vector (Normalize module) */
 } hcr_bert_config;
 typedef struct hcr_encoder hcr_encoder;
-/* compute_dtype: HCR_F16 or HCR_BF16 (MFMA operands; accumulation, LayerNorm, softmax and
- * the residual stream are fp32). */
+/* compute_dtype:
+ *   HCR_F32  reference precision (the reference encodes in fp32 torch,
+ *            experiments/embedding_generator.py:124): projection GEMMs as three-term split-f16
+ *            MFMA products (~22-bit operands, fp32 accumulation), fp32 attention/softmax/
+ *            LayerNorm/residual; matches fp32 BertModel to ~1e-6;
+ *   HCR_F16 / HCR_BF16  fast: f16 / bf16 MFMA operands (accumulation, LayerNorm, softmax and
+ *            the residual stream fp32). */
 int hcr_encoder_create(int device, const hcr_bert_config* cfg, int compute_dtype,
                        hcr_encoder** out);
+int hcr_encoder_compute_dtype(const hcr_encoder* enc);
 int hcr_encoder_destroy(hcr_encoder* enc);
 /* HF BertModel state-dict tensor (fp32, row-major as stored).  Any prefix before
  * "embeddings." / "encoder." is ignored; pooler / head tensors are accepted and unused. */
