@@ -1,12 +1,16 @@
 """Headline benchmark (BASELINE.json): brute-force cosine top-k QPS over a 10M x 768 fp16
-node-embedding corpus, batch 1024 queries, top-32 (configs[2]), on 1..8 MI355X.
+node-embedding corpus, batch 1024 queries, top-32 (configs[2]), on 1..8 MI355X, plus the
+query-embedding throughput of the encoder in both compute modes.
 
-One process per GPU (torchrun sets RANK / LOCAL_RANK / WORLD_SIZE).  Weak scaling: the 10M
-corpus is row-sharded over W GPUs and the query batch is 1024 per GPU, so every GPU scores
-the same (rows x queries) work as the 1-GPU run:
-    all-gather(query embeddings)  ->  local fused MFMA score + top-k' + fp64 rescore on the
-    shard  ->  all-to-all(per-shard exact top-k)  ->  on-device merge of W lists per query.
-A step = one such pass over one batch (queries already resident in HBM).
+One process per GPU (torchrun sets RANK / LOCAL_RANK / WORLD_SIZE; `bench.py --gpus N` without
+torchrun launches its own N ranks through torch.distributed.run before touching the GPU).
+Strong scaling (the metric: a fixed 10M corpus and a fixed global batch of 1024 queries on
+1/2/4/8 GPUs; --global-batch 4096 at 8 GPUs is configs[3]): the corpus is row-sharded over W
+GPUs, each rank holds global_batch / W queries, and one step is
+    all-gather(query embeddings)  ->  local fused MFMA score + top-k' + fp64 rescore of all
+    global_batch queries on the shard  ->  all-to-all(per-shard exact top-k)  ->  on-device
+    merge of W lists per own query,
+with the queries already resident in HBM.  `value` = global_batch / (max-over-ranks step time).
 
 Prints ONE JSON line on rank 0 (the driver's contract); diagnostics go to stderr.
 """
@@ -39,7 +43,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--rows", type=int, default=10_000_000)
     p.add_argument("--dim", type=int, default=768)
-    p.add_argument("--batch", type=int, default=1024, help="queries per GPU per step")
+    p.add_argument("--global-batch", type=int, default=1024,
+                   help="queries per step over all GPUs (strong scaling; configs[3]: 4096)")
+    p.add_argument("--batch", type=int, default=0,
+                   help="queries per GPU per step (weak scaling; overrides --global-batch)")
     p.add_argument("--k", type=int, default=32)
     p.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
@@ -47,13 +54,44 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--encoder", default="bge-base", choices=["bge-base", "bge-large", "minilm", "none"],
                    help="query-embedding leg: BERT shape (random init) encoded on each GPU")
+    p.add_argument("--enc-modes", default="f32,f16",
+                   help="encoder compute modes to time: f32 (reference precision) and/or f16/bf16")
     p.add_argument("--enc-seq", type=int, default=32)
     p.add_argument("--enc-steps", type=int, default=10)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_score.json"),
                    help="PMC HBM-traffic summary (tools/pmc_summary.py --traffic) of this config")
-    p.add_argument("--sweep", default="", help="comma list of batch sizes for an extra "
-                   "1-GPU sweep printed to stderr (e.g. 1,8,32,64,256,1024)")
+    p.add_argument("--sweep", default="1,8,32,64,256",
+                   help="batch sizes of the 1-GPU small-batch sweep recorded in extra.batch_sweep "
+                        "('' to skip)")
     return p.parse_args()
+
+
+def spawn_ranks(a):
+    """`bench.py --gpus N` outside torchrun: launch N ranks (torch.distributed.run, 127.0.0.1)
+    as a child process -- before this process touches the GPU -- and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    log(f"spawning {a.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def make_shard(ix, hc, r0, r1, dim, dtype, dev, seed=1000, chunk=1 << 20):
@@ -85,11 +123,20 @@ def make_queries(ix_rows_fn, B, dim, dev, rank, n_local, r0):
     return Q, (src_local + r0)
 
 
-def workload_name(N, D, dtype, B, k, world):
+def workload_name(N, D, dtype, GB, k, world):
     """Names the BASELINE.json config a run matches (configs[2] is the default headline)."""
-    tag = {(10_000_000, 768, 1024, 32): "configs[2]", (1_000_000, 384, 256, 10): "configs[1]",
-           (100_000_000 // 8, 1024, 1024, 64): "configs[4] per-rank shape"}.get((N, D, B, k), "custom")
-    return (f"{tag}: {N:,} x {D} {dtype} node embeddings, batch={B} queries per GPU, top-{k} "
+    key = (N, D, GB, k)
+    if key == (10_000_000, 768, 1024, 32):
+        tag = "configs[2]" if world == 1 else "metric strong-scaling point (configs[2] corpus and batch)"
+    elif key == (10_000_000, 768, 4096, 32):
+        tag = "configs[3]" if world == 8 else "configs[3] corpus and batch"
+    elif key == (1_000_000, 384, 256, 10):
+        tag = "configs[1]"
+    elif key == (100_000_000 // 8, 1024, 8192, 64):
+        tag = "configs[4] per-rank shape"
+    else:
+        tag = "custom"
+    return (f"{tag}: {N:,} x {D} {dtype} node embeddings, global batch={GB} queries, top-{k} "
             f"(row-sharded over {world} GPU{'s' if world > 1 else ''})")
 
 
@@ -109,9 +156,10 @@ def load_traffic(path, N, D, nq, k, dtype, world):
 
 
 def cpu_baseline(E_rows_f16, Q, k, n_total):
-    """Oracle ("port") timed on the host: the reference's literal path — sklearn-semantics
+    """Oracle ("port") timed on the host: the reference's literal path -- sklearn-semantics
     cosine in fp64 over the fp64 matrix + np.argsort(...)[::-1][:k] (experiments/main.py:
-    841-844) — on a bounded sample, extrapolated linearly in rows."""
+    841-844) -- on a bounded sample, extrapolated linearly in rows; beside it the tuned CPU
+    path of BASELINE.md §3 (fp32 BLAS GEMM + argpartition) on the same sample."""
     from oracle import cosine_topk as O
     E = E_rows_f16.astype(np.float64)
     q = Q.astype(np.float64)
@@ -122,12 +170,28 @@ def cpu_baseline(E_rows_f16, Q, k, n_total):
     del top, sims
     nq, nr = Q.shape[0], E.shape[0]
     qps = nq / (t * (n_total / nr))
+    # tuned: fp32 unit rows (normalised once, outside the timed region, as an index would
+    # store them), one SGEMM, argpartition + a sort of the k survivors
+    E32 = (E / np.linalg.norm(E, axis=1, keepdims=True)).astype(np.float32)
+    q32 = Q.astype(np.float32)
+    del E
+    t1 = time.perf_counter()
+    s32 = (q32 / np.linalg.norm(q32, axis=1, keepdims=True)) @ E32.T
+    part = np.argpartition(-s32, k, axis=1)[:, :k]
+    np.take_along_axis(s32, part, axis=1).argsort(axis=1)
+    tt = time.perf_counter() - t1
+    del s32, E32
     threads = int(os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
                   or os.cpu_count() or 1)
     return {"value": qps, "unit": "queries/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "threads_env": {v: os.environ.get(v) for v in (
+                "OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")},
             "sample": f"{nq} queries x {nr:,}-row slice of the same corpus (fp16 decoded to fp64), "
                       f"cosine_similarity fp64 + argsort[::-1][:{k}] in {t:.2f} s, "
-                      f"extrapolated linearly to {n_total:,} rows"}
+                      f"extrapolated linearly to {n_total:,} rows",
+            "tuned": {"value": nq / (tt * (n_total / nr)), "unit": "queries/s",
+                      "path": "fp32 SGEMM over pre-normalised rows + argpartition (BASELINE.md §3)",
+                      "seconds_on_sample": round(tt, 3)}}
 
 
 ENC_SHAPES = {
@@ -167,13 +231,15 @@ def random_bert_state(cfg, seed=0):
     return sd
 
 
-def encoder_leg(a, hc, dev, rank, world, dist):
-    """Query-embedding throughput: B query token sequences (S = --enc-seq, ragged lengths)
-    -> BERT forward -> pool -> L2 on each GPU; whole-job embeddings/s over max-over-ranks
-    time.  FLOPs per query = 2 * P_nonemb * S + 4 * L * S^2 * H."""
+def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
+    """Query-embedding throughput of one compute mode: B query token sequences per rank
+    (S = --enc-seq, ragged lengths) -> BERT forward -> pool -> L2; whole-job embeddings/s over
+    the max-over-ranks time.  Useful FLOPs per query = 2 * P_nonemb * S + 4 * L * S^2 * H
+    (SURVEY.md §8(d)); the reference-precision mode executes 3x the projection FLOPs on MFMA
+    (three split-f16 terms), reported as mfma_frac_executed."""
     cfg = ENC_SHAPES[a.encoder]
-    enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=a.dtype, device=dev.index)
-    B, S = a.batch, a.enc_seq
+    enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=mode, device=dev.index)
+    S = a.enc_seq
     g = torch.Generator(device="cpu").manual_seed(77 + rank)
     ids = torch.randint(1000, cfg["vocab_size"], (B, S), generator=g, dtype=torch.int32)
     lens = torch.randint(S // 2, S + 1, (B,), generator=g)
@@ -204,18 +270,64 @@ def encoder_leg(a, hc, dev, rank, world, dist):
     flops_q = 2.0 * p_nonemb * S + 4.0 * L * S * S * H
     per_step = el / a.enc_steps
     tf = B * flops_q / per_step / 1e12
+    gemm_mult = 3.0 if mode == "f32" else 1.0
+    tf_exec = B * (gemm_mult * 2.0 * p_nonemb * S) / per_step / 1e12
     norms = out.norm(dim=1)
     enc.close()
-    return {"model": f"{a.encoder} shape, random init", "seq_len": S, "batch_per_gpu": B,
+    return {"mode": mode,
+            "precision": ("reference (split-f16 MFMA GEMMs, fp32 attention; max |diff| vs fp32 "
+                          "BertModel ~1e-6, tests/test_encoder_gpu.py)" if mode == "f32"
+                          else f"fast ({mode} MFMA operands, fp32 accumulation)"),
+            "model": f"{a.encoder} shape, random init", "seq_len": S, "batch_per_gpu": B,
             "query_embeddings_per_s": round(world * B / per_step, 1),
-            "ms_per_batch": round(per_step * 1e3, 3), "gpu_ms_per_batch": round(ev0.elapsed_time(ev1) / a.enc_steps, 3),
+            "ms_per_batch": round(per_step * 1e3, 3),
+            "gpu_ms_per_batch": round(ev0.elapsed_time(ev1) / a.enc_steps, 3),
             "flops_per_query": flops_q, "TFLOPs": round(tf, 2),
             "mfma_frac": round(tf / MFMA_PEAK_TFLOPS, 4),
+            "mfma_frac_executed": round(tf_exec / MFMA_PEAK_TFLOPS, 4),
             "unit_norm_ok": bool(((norms - 1).abs() < 1e-3).all().item())}
+
+
+def batch_sweep(a, ix, dev, nloc, D, k):
+    """Small-batch sweep on rank 0 (1 GPU): the HBM-bound regime of north_star (B <= 64 on the
+    headline corpus).  Per batch: wall time of one search (queries in HBM), the score kernel's
+    HIP-event time, and both as fractions of the 8 TB/s HBM roofline on the algorithmic bytes."""
+    out = []
+    stream = torch.cuda.current_stream().cuda_stream
+    for bsz in [int(x) for x in a.sweep.split(",") if x]:
+        g = torch.Generator(device=dev).manual_seed(900 + bsz)
+        Qs = torch.randn((bsz, D), device=dev, generator=g)
+        Ss = torch.empty((bsz, k), dtype=torch.float64, device=dev)
+        Is = torch.empty((bsz, k), dtype=torch.int64, device=dev)
+        for _ in range(2):
+            ix.search_device(Qs.data_ptr(), bsz, k, Ss.data_ptr(), Is.data_ptr(), stream=stream)
+        ix.set_timing(True)
+        torch.cuda.synchronize()
+        reps = 10
+        ts = time.perf_counter()
+        km = 0.0
+        for _ in range(reps):
+            ix.search_device(Qs.data_ptr(), bsz, k, Ss.data_ptr(), Is.data_ptr(), stream=stream)
+            km += ix.last_stats()["score_kernel_ms"]
+        torch.cuda.synchronize()
+        te = (time.perf_counter() - ts) / reps
+        ix.set_timing(False)
+        kms = km / reps
+        byt = nloc * D * 2 + bsz * D * 2 + bsz * k * 12
+        fl = 2.0 * bsz * nloc * D
+        out.append({"batch": bsz, "qps": round(bsz / te, 1), "ms_per_batch": round(te * 1e3, 4),
+                    "kernel_ms": round(kms, 4),
+                    "hbm_frac_batch": round(byt / te / 1e9 / HBM_PEAK_GBS, 4),
+                    "hbm_frac_kernel": round(byt / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "kernel_TFLOPs": round(fl / (kms * 1e-3) / 1e12, 2)})
+        log(json.dumps({"sweep": out[-1]}))
+    return out
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -229,7 +341,14 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import hcrag_amd as hc
-    N, D, B, k = a.rows, a.dim, a.batch, a.k
+    N, D, k = a.rows, a.dim, a.k
+    if a.batch > 0:                         # weak scaling: a fixed batch per GPU
+        B, scaling = a.batch, "weak"
+    else:                                   # strong scaling: a fixed global batch
+        if a.global_batch % world:
+            raise SystemExit(f"--global-batch {a.global_batch} not divisible by {world} GPUs")
+        B, scaling = a.global_batch // world, "strong"
+    nq = world * B                          # queries scored by every shard per step
     from hcrag_amd.distributed import shard_range
     r0, r1 = shard_range(N, rank, world)
     nloc = r1 - r0
@@ -247,7 +366,6 @@ def main():
         return torch.stack(out).to(dev)
 
     Q, src = make_queries(rows_fn, B, D, dev, rank, nloc, r0)
-    nq = world * B
     from hcrag_amd.distributed import ShardedSearch, hip_local_search, hip_merge
     searcher = ShardedSearch(hip_local_search(ix, k), hip_merge(k), k)
 
@@ -259,7 +377,7 @@ def main():
     torch.cuda.synchronize()
 
     ix.set_timing(True)
-    kern_ms, launches, unc, widened = 0.0, 0, 0, 0
+    kern_ms, launches, unc, widened, fallback = 0.0, 0, 0, 0, 0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -271,6 +389,7 @@ def main():
         launches += st["score_launches"]
         unc += st["uncertified_queries"]
         widened += st["widened_queries"]
+        fallback += st["fallback_queries"]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -301,7 +420,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None}
     roof["traffic"] = load_traffic(a.traffic_file, N, D, nq, k, a.dtype, world)
-    roof["traffic_unit"] = "GB per score phase (rocprofv3 FETCH_SIZE+WRITE_SIZE, profiles/traffic_score.json)"
+    roof["traffic_unit"] = ("GB per score phase (rocprofv3 FETCH_SIZE+WRITE_SIZE passes of this "
+                            "config, profiles/traffic_score.json)")
     roof["kernel"] = ("score_topk_v4_kernel (fused MFMA score + top-k'): sample pre-pass + "
                       "dense pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
@@ -326,55 +446,36 @@ def main():
 
     enc_res = None
     if a.encoder != "none":
-        enc_res = encoder_leg(a, hc, dev, rank, world, dist)
+        enc_res = {}
+        for mode in [m for m in a.enc_modes.split(",") if m]:
+            enc_res[mode] = encoder_leg(a, hc, dev, rank, world, dist, mode, B)
 
+    sweep = None
     if a.sweep and world == 1 and rank == 0:
-        for bsz in [int(x) for x in a.sweep.split(",") if x]:
-            Qs = torch.randn((bsz, D), device=dev)
-            Ss = torch.empty((bsz, k), dtype=torch.float64, device=dev)
-            Is = torch.empty((bsz, k), dtype=torch.int64, device=dev)
-            stream = torch.cuda.current_stream().cuda_stream
-            for _ in range(2):
-                ix.search_device(Qs.data_ptr(), bsz, k, Ss.data_ptr(), Is.data_ptr(), stream=stream)
-            ix.set_timing(True)
-            torch.cuda.synchronize()
-            ts = time.perf_counter()
-            km = 0.0
-            reps = 5
-            for _ in range(reps):
-                ix.search_device(Qs.data_ptr(), bsz, k, Ss.data_ptr(), Is.data_ptr(), stream=stream)
-                km += ix.last_stats()["score_kernel_ms"]
-            torch.cuda.synchronize()
-            te = (time.perf_counter() - ts) / reps
-            ix.set_timing(False)
-            kms = km / reps
-            byt = nloc * D * 2 + bsz * D * 2
-            fl = 2.0 * bsz * nloc * D
-            log(json.dumps({"sweep_batch": bsz, "qps": bsz / te, "ms_per_batch": te * 1e3,
-                            "kernel_ms": kms, "kernel_hbm_GBs": byt / (kms * 1e-3) / 1e9,
-                            "kernel_TFLOPs": fl / (kms * 1e-3) / 1e12}))
+        sweep = batch_sweep(a, ix, dev, nloc, D, k)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "scaling": scaling, "vs_baseline": None, "dtype": a.dtype,
             "data": "synthetic: N(0,1) rows L2-normalised at ingest then rounded to fp16; "
                     "queries 50% planted (corpus row + noise) / 50% random, fp32, HBM-resident",
-            "config": {"workload": workload_name(N, D, a.dtype, B, k, world),
+            "config": {"workload": workload_name(N, D, a.dtype, nq, k, world),
                        "rows": N, "dim": D, "batch_per_gpu": B, "global_batch": nq, "k": k,
                        "parallelism": f"rowshard{world}" + ("+rccl_allgather_alltoall" if world > 1 else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "encoder": enc_res,
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
-                      "widened_queries": widened, "kprime": st["kprime"],
-                      "unit_kernel": st["unit_kernel"],
+                      "widened_queries": widened, "fallback_queries": fallback,
+                      "kprime": st["kprime"], "unit_kernel": st["unit_kernel"],
                       "partitions": st["partitions"], "workgroups": st["workgroups"],
                       "mfma_frac": round(flops / (avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
                       "hbm_frac_kernel": round(bytes_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                      "pipeline_ms_per_step": round(elapsed / a.steps * 1e3, 3)},
+                      "pipeline_ms_per_step": round(elapsed / a.steps * 1e3, 3),
+                      "batch_sweep": sweep},
         }
         print(json.dumps(line), flush=True)
     ix.close()
