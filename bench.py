@@ -60,6 +60,8 @@ def parse():
     p.add_argument("--enc-steps", type=int, default=10)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_score.json"),
                    help="PMC HBM-traffic summary (tools/pmc_summary.py --traffic) of this config")
+    p.add_argument("--no-configs0", action="store_true",
+                   help="skip the configs[0] real-data leg (GPU vs CPU on data/Product*.csv)")
     p.add_argument("--sweep", default="1,8,32,64,256",
                    help="batch sizes of the 1-GPU small-batch sweep recorded in extra.batch_sweep "
                         "('' to skip)")
@@ -288,6 +290,65 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
             "unit_norm_ok": bool(((norms - 1).abs() < 1e-3).all().item())}
 
 
+def configs0_leg(hc):
+    """BASELINE.json configs[0] on the reference's own data: the 441 graph_builder.py:224-284
+    documents of data/Product*.csv (committed fixture tests/golden/configs0/), MiniLM-shape
+    encoder (seeded weights; no checkpoints offline), node index, top-5 / threshold 0.3 for the
+    queries of experiments/main.py:1179-1184.  GPU: WordPiece + reference-precision encoder +
+    EmbeddingSearch.  CPU, same run, same host: the reference's engines restated (HF Rust
+    tokenizer + transformers BertModel fp32 in batches of 10 as HuggingFaceEmbedding's
+    embed_batch_size, then sklearn cosine + argsort per query).  Times exclude model loading."""
+    import gzip
+    gdir = os.path.join(ROOT, "tests", "golden", "configs0")
+    if not os.path.exists(os.path.join(gdir, "goldens.json")):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_configs0 import cpu_reference_embed
+    from oracle import cosine_topk as O
+    from hcrag_amd.synthetic import bert_state
+    with gzip.open(os.path.join(gdir, "texts.jsonl.gz"), "rt", encoding="utf-8") as fh:
+        docs = [json.loads(line) for line in fh]
+    with open(os.path.join(gdir, "goldens.json")) as fh:
+        gold = json.load(fh)
+    texts = [d["text"] for d in docs]
+    cfg = dict(gold["model"])
+    state = bert_state(cfg, seed=gold["seed"], perturb_ln=gold["perturb_ln"])
+    vocab = os.path.join(gdir, "vocab.txt")
+    tok = hc.WordPieceTokenizer(vocab, lowercase=True)
+    emb = hc.SentenceEmbedder(tok, hc.BertEncoder(cfg, state, dtype="f32"),
+                              max_seq_length=gold["max_seq_length"], batch_size=64)
+    emb.encode(texts[:8])                                  # warm-up (kernel load)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    E = emb.encode(texts)
+    srch = hc.EmbeddingSearch(E, texts, [d["metadata"] for d in docs], dtype="f32", embedder=emb)
+    gpu_res = [srch.find_similar_content(q, top_k=gold["top_k"], similarity_threshold=gold["threshold"])
+               for q in gold["queries"]]
+    t_gpu = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    Ec = cpu_reference_embed(texts, vocab, state, cfg, batch=10)
+    cpu_res = []
+    for q in gold["queries"]:
+        qe = cpu_reference_embed([q], vocab, state, cfg, batch=1)[0]
+        cpu_res.append(O.find_similar_content(qe, Ec.astype(np.float64), gold["top_k"], gold["threshold"]))
+    t_cpu = time.perf_counter() - t1
+    same = all([texts.index(x["content"]) for x in g] == [i for i, _ in c]
+               for g, c in zip(gpu_res, cpu_res))
+    dmax = max(abs(x["similarity_score"] - sc) for g, c in zip(gpu_res, cpu_res)
+               for x, (_, sc) in zip(g, c))
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    return {"workload": "configs[0]: data/Product*.csv (441 graph_builder.py documents) -> "
+                        "MiniLM-shape encoder (seeded) -> vector top-5, threshold 0.3, 4 queries "
+                        "(experiments/main.py:1179-1184)",
+            "gpu_s": round(t_gpu, 4), "cpu_s": round(t_cpu, 4), "speedup": round(t_cpu / t_gpu, 1),
+            "gpu_texts_per_s": round(len(texts) / t_gpu, 1), "cpu_texts_per_s": round(len(texts) / t_cpu, 1),
+            "cpu_cores": threads, "cpu_model": cpu_model(), "ids_identical": bool(same),
+            "max_score_diff": float(dmax),
+            "gpu_path": "hcr_tokenize + hcr_encode (f32 reference precision) + hcr_search",
+            "cpu_path": "HF tokenizers + transformers BertModel fp32 (batches of 10) + sklearn-"
+                        "semantics cosine + argsort (oracle)"}
+
+
 def batch_sweep(a, ix, dev, nloc, D, k):
     """Small-batch sweep on rank 0 (1 GPU): the HBM-bound regime of north_star (B <= 64 on the
     headline corpus).  Per batch: wall time of one search (queries in HBM), the score kernel's
@@ -453,6 +514,9 @@ def main():
     sweep = None
     if a.sweep and world == 1 and rank == 0:
         sweep = batch_sweep(a, ix, dev, nloc, D, k)
+    c0 = None
+    if rank == 0 and world == 1 and not a.no_configs0:
+        c0 = configs0_leg(hc)
 
     if rank == 0:
         line = {
@@ -468,6 +532,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "encoder": enc_res,
+            "configs0": c0,
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
                       "widened_queries": widened, "fallback_queries": fallback,
                       "kprime": st["kprime"], "unit_kernel": st["unit_kernel"],

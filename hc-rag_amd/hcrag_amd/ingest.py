@@ -128,6 +128,51 @@ def flatten_json_to_text(obj, prefix: str = "") -> List[str]:
     return out
 
 
+def read_csv_like_graph_builder(path):
+    """graph_builder.py:228-248: the first (separator, encoding) among ``, ; \\t |`` x
+    ``utf-8 latin-1 cp1252`` that pandas parses into more than one column (the reference tries
+    "," first, so a ";"-separated file with decimal commas is split on its commas), else None."""
+    import pandas as pd
+    df = None
+    for sep in (",", ";", "\t", "|"):
+        for enc in ("utf-8", "latin-1", "cp1252"):
+            try:
+                df = pd.read_csv(path, sep=sep, encoding=enc)
+                if len(df.columns) > 1:
+                    break
+            except Exception:
+                continue
+        if df is not None and len(df.columns) > 1:
+            break
+    if df is None or len(df.columns) <= 1:
+        return None
+    return df
+
+
+def csv_record_documents(path, file_name: Optional[str] = None) -> List[Dict[str, Any]]:
+    """The documents ``GraphBuilder._process_csv_content`` makes of a CSV (graph_builder.py:
+    224-284): per row "Record from {file}:" then "col: value" for every non-null, non-blank
+    cell, joined by ". ", with metadata source / source_type / row_index / columns and id
+    ``{file}_row_{idx}``.  These texts are what ``PropertyGraphIndex.from_documents`` embeds into
+    the SimplePropertyGraphStore path of BASELINE.json configs[0]."""
+    import pandas as pd
+    name = file_name or Path(path).name
+    df = read_csv_like_graph_builder(path)
+    if df is None:
+        return []
+    docs = []
+    for idx, row in df.iterrows():
+        parts = [f"Record from {name}:"]
+        for col, value in row.items():
+            if pd.notna(value) and str(value).strip():
+                parts.append(f"{col}: {value}")
+        if len(parts) > 1:
+            docs.append({"id": f"{name}_row_{idx}", "text": ". ".join(parts),
+                         "metadata": {"source": name, "source_type": "csv", "row_index": int(idx),
+                                      "columns": [str(c) for c in row.keys()]}})
+    return docs
+
+
 class BatchedEmbeddingGenerator:
     """``DynamicEmbeddingGenerator`` surface with batched GPU encoding.
 
@@ -240,4 +285,4 @@ class BatchedEmbeddingGenerator:
 
 
 __all__ = ["EmbeddingStore", "BatchedEmbeddingGenerator", "analyze_data_patterns", "smart_text",
-           "flatten_json_to_text"]
+           "flatten_json_to_text", "csv_record_documents", "read_csv_like_graph_builder"]
