@@ -25,25 +25,9 @@
 
 using namespace hcr;
 
-// ---------------------------------------------------------------------------------------
-// errors
-// ---------------------------------------------------------------------------------------
-static thread_local std::string g_err;
+#define set_err hcr_set_errorf     // errors.cpp: thread-local message + status code
 
-int hcr_set_errorf(int code, const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-#define set_err hcr_set_errorf
-
-extern "C" const char* hcr_last_error(void) { return g_err.c_str(); }
-int hcr_set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
-extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.1.0 (gfx950)"; }
+extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.2.0 (gfx950)"; }
 extern "C" int hcr_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

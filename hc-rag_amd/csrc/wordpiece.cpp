@@ -22,7 +22,7 @@
 #include "hcrag.h"
 #include "unicode_tables.h"
 
-extern int hcr_set_error(int code, const char* msg);   // hcrag_index.hip
+extern int hcr_set_error(int code, const char* msg);   // errors.cpp
 
 namespace {
 

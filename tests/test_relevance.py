@@ -119,3 +119,43 @@ def test_batch_isrelevant_dropin():
         return [0.5] * len(batch)
     G.batch_isRelevant(q, nodes, G.ScorerType.ROUTER, batch_size=8, llm_judge=judge)
     assert judge_calls == [8, 8, 4]                                   # isRelevant.py:523-527
+
+
+def _ka():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "isrelevant_known_answers.json")) as f:
+        return json.load(f)
+
+
+def test_reference_known_answers_oracle():
+    """The reference's own isRelevant vectors (test_milestone1:177-263) through the oracle."""
+    ka = _ka()
+    em = ka["entity_match"]
+    got = [R.entity_match(em["query_entities"], n["entities"]) for n in em["nodes"]]
+    for g, e, t in zip(got, em["expected"], em["tolerance"]):
+        assert abs(g - e) <= t
+    tp = ka["node_type_priority"]
+    assert [R.node_type_priority(tp["intent"], n["node_type"]) for n in tp["nodes"]] == tp["expected"]
+
+
+@pytest.mark.gpu
+def test_reference_known_answers_gpu():
+    """The same vectors through hcr_relevance_combine (batch_entity_match /
+    batch_node_type_priority run the GPU kernel)."""
+    from types import SimpleNamespace as NS
+    from hcrag_amd import relevance as G
+    ka = _ka()
+    rng = np.random.default_rng(0)
+    for key, fn in (("entity_match", G.batch_entity_match),
+                    ("node_type_priority", G.batch_node_type_priority)):
+        c = ka[key]
+        q = NS(text="Find red mountain bikes", embeddings=rng.random(384),
+               entities=c["query_entities"], intent=G.QueryIntent(c["intent"]))
+        nodes = [NS(text=n["text"], embeddings=rng.random(384), graph_relations={},
+                    node_type=n["node_type"], entities=n["entities"]) for n in c["nodes"]]
+        got = fn(q, nodes)
+        tol = c.get("tolerance", [0.0] * len(got))
+        assert len(got) == len(c["expected"])
+        for g, e, t in zip(got, c["expected"], tol):
+            assert abs(g - e) <= t, (key, got)
