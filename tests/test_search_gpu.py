@@ -422,7 +422,7 @@ def test_llama_vector_store_dropin(hc):
     sims, ids = O.llama_get_top_k_embeddings(q.astype(np.float32), E.astype(np.float32), 10,
                                              [f"n{r}" for r in range(N)])
     assert res.ids == ids
-    np.testing.assert_allclose(res.similarities, sims, atol=1e-6)
+    np.testing.assert_allclose(res.similarities, sims, atol=1e-12)
     flt = SimpleNamespace(filters=[SimpleNamespace(key="type", value="b", operator="==")])
     res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=5, filters=flt))
     keep = [r for r in range(N) if r % 4 == 0]
