@@ -472,3 +472,33 @@ def test_prepass_seed_parity(env):
                        env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "parity ok" in r.stdout
+
+
+def test_configs4_rank_shape_bf16(hc):
+    """configs[4]'s per-rank shape (100M x 1024 bf16 over 8 GPUs, global batch 8192, top-64):
+    bf16 rows, D = 1024, k = 64, nq = 8192 on one shard (rows reduced to 40k so the oracle
+    finishes; 64 queries of it checked exactly, planted recall on all)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(1024)
+    N, D, B, k = 40000, 1024, 8192, 64
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    planted = rng.integers(0, N, B // 2)
+    Q[::2] = E[planted] + 0.05 * rng.standard_normal((B // 2, D)).astype(np.float32)
+    dev = torch.device("cuda:0")
+    with hc.VectorIndex(D, "bf16", capacity=N) as ix:
+        ix.add(E, normalize=True)
+        ix.set_id_offset(3 * N)                       # a rank's shard offset
+        q = torch.from_numpy(Q).to(dev)
+        S = torch.empty((B, k), dtype=torch.float64, device=dev)
+        I = torch.empty((B, k), dtype=torch.int64, device=dev)
+        ix.search_device(q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(),
+                         stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert ix.last_stats()["uncertified_queries"] == 0
+        S, I = S.cpu().numpy(), I.cpu().numpy()
+        R = ix.get_rows()
+    assert np.mean(I[::2, 0] - 3 * N == planted) > 0.99
+    sub = np.r_[0:32, B - 32:B]
+    es, ei = O.cosine_topk(Q[sub], R, k)
+    _check(S[sub], I[sub] - 3 * N, es, ei, tol=SCORE_TOL_F64)
