@@ -22,6 +22,7 @@
 #include "topk_kernels.h"
 #include "score_v3.h"
 #include "score_v4.h"
+#include "score_qs_launch.h"
 
 using namespace hcr;
 
@@ -55,7 +56,7 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt, w_tauest, w_umax, w_sk;
+      w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again;
   hcr_search_stats stats{};
@@ -128,6 +129,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
                    &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax, &ix->w_sk,
+                   &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again};
   for (DevBuf* b : all) b->release();
@@ -406,7 +408,8 @@ extern "C" int hcr_index_last_stats(const hcr_index* ix, hcr_search_stats* out) 
 // ---------------------------------------------------------------------------------------
 static int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 static constexpr int kMaxKprime = 512;
-static constexpr int kMergeMaxKeys = 8192;      // 64 KiB of LDS in merge_partials_kernel
+static constexpr int kMergeMaxKeys = 16384;     // keys per merge_lists_kernel block (128 KiB of
+                                                // LDS): one level for P x k' <= 256 x 64
 static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
@@ -418,7 +421,7 @@ static void launch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipS
                      ix->rows.as<const TS>(), ix->ld, ix->n, ix->ld / BK, ix->inv32.as<const float>(),
                      ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                      ix->w_qhat.as<const TM>(), nqb, P, ntiles, ix->w_buf.as<uint64_t>(),
-                     ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), kp);
+                     ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), kp);
 }
 
 template <typename TS, typename TM>
@@ -446,8 +449,10 @@ static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_c
 //   HCRAG_RIGOROUS_SEED     seed rank j = k' (rigorous) instead of the estimate
 //   HCRAG_SEED_RANK         force seed rank j (aggressive seeds exercise the re-runs)
 //   HCRAG_PREPASS_TOPK      the top-k' pre-pass form instead of MAXONLY
+//   HCRAG_QS_MAX            largest batch on the query-stationary kernel (0: off)
 struct TestHooks {
   int64_t q64_elems = kQ64WideMaxElems;
+  int qs_max = 128;
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
@@ -455,6 +460,7 @@ static const TestHooks& hooks() {
   static const TestHooks h = [] {
     TestHooks t;
     if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
+    if (const char* e = getenv("HCRAG_QS_MAX")) t.qs_max = atoi(e);
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
@@ -466,20 +472,25 @@ static const TestHooks& hooks() {
   return h;
 }
 
-struct V3Cfg { int rt, qt, nst; };
+struct V3Cfg { int rt, qt, nst; bool qs; };   // qs: query-stationary kernel (score_qs.h)
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
-  if (nq <= 16) return {256, 16, 8};
+  if (nq <= 16) return {256, 16, 8, false};
+  // 17-128 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
+  // LDS).  r02j (gpurun_out/r02j_*, score ms QS vs v3/v4): 10M x 768 B = 32 2.85 vs 3.69,
+  // B = 128 3.02 vs 4.23, B = 256 (two query blocks) 5.03 vs 4.53; 1M x 384 B = 32 0.215 vs
+  // 0.276, B = 256 0.348 vs 0.313 -> 256 x 256 (v4) from 129 queries.
+  if (nq <= hooks().qs_max && qs_supported(ld)) return {kQsRowTile, 128, 4, true};
   // 17-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
   // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
   // 1M x 768 0.49 vs 0.52, 2.5M x 768 1.11 vs 1.08, 5M x 768 2.13 vs 1.98, 10M x 768 4.13 vs
   // 3.73 -> the crossover is between 0.8e9 and 1.9e9 corpus elements (the cost of either tile
   // shape is flat in the batch within its range).
-  if (nq <= 64 && n_rows * (int64_t)ld <= hooks().q64_elems) return {256, 256, 4};
-  if (nq <= 64) return {256, 64, 7};
+  if (nq <= 64 && n_rows * (int64_t)ld <= hooks().q64_elems) return {256, 256, 4, false};
+  if (nq <= 64) return {256, 64, 7, false};
   // 65+ queries: the 256 x 256 kernel (v4), also for 65-128 where half its query columns are
   // padding (MAXONLY pre-pass + UNIT epilogue; r01g sweeps: 10M x 768 B = 200 4.51 ms vs
   // B = 128 4.74 ms on 256 x 128; 1M x 384 0.31 vs 0.57 ms)
-  return V3Cfg{256, 256, 4};
+  return V3Cfg{256, 256, 4, false};
 }
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
@@ -510,7 +521,15 @@ static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
                      ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                      ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
                      ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                     ix->w_part.as<uint64_t>(), a.kp);
+                     ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp);
+}
+
+static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
+  QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(),
+           ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr, ix->w_qhat.p, a.nqb, a.P,
+           a.nvt, a.tstride, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit};
+  return launch_qs(ix->dtype, q, st);
 }
 
 template <typename TM, int CAP>
@@ -523,7 +542,7 @@ static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
                          ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                          ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
                          ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                         ix->w_part.as<uint64_t>(), a.kp);
+                         ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp);
     else
       hipLaunchKernelGGL((score_topk_v4_kernel<TM, CAP, 4, false>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                          ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
@@ -531,7 +550,7 @@ static int launch_v3_cap(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
                          ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                          ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
                          ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-                         ix->w_part.as<uint64_t>(), a.kp);
+                         ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp);
   }
   else if (c.qt == 64) launch_v3_t<TM, CAP, 256, 64, 4, 2, 7>(ix, a, st);
   else launch_v3_t<TM, CAP, 256, 16, 8, 1, 8>(ix, a, st);
@@ -548,20 +567,21 @@ static int launch_v4_maxonly(hcr_index* ix, V3Launch a, hipStream_t st) {
                        ix->inv32.as<const float>(),
                        ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                        ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
-                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, a.kp);
+                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, nullptr, a.kp);
   else
     hipLaunchKernelGGL((score_topk_v4_kernel<TM, 512, 4, false, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                        st, ix->rows.as<const TM>(), ix->ld, ix->n, ix->ld / V3_BK,
                        ix->inv32.as<const float>(),
                        ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,
                        ix->w_qhat.as<const TM>(), a.nqb, a.P, a.nvt, a.tstride,
-                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, a.kp);
+                       ix->w_umax.as<uint64_t>(), ix->w_taug.as<uint32_t>(), nullptr, nullptr, a.kp);
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
 template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
+  if (c.qs) return launch_qs_ix(ix, c, a, st);              // CAP chosen in score_qs.hip
   switch (cap) {
     case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
     case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
@@ -623,28 +643,50 @@ seed_from_maxima_kernel(const float* __restrict__ umax, int U, int nqpad, int j,
   }
 }
 
-// Tree merge of the per-partition lists in ix->w_part ([q][P][kp]) into one sorted top-kp list
-// per query ([q][kp]); groups of G lists per block, ping-ponging through ix->w_merged.
-static int merge_tree(hcr_index* ix, int nq, int nqpad, int P, int P2, int G, int kp,
-                      hipStream_t st, const uint64_t** out) {
+// Tree merge of the per-partition lists in ix->w_part ([q][P][kp] slots, counts in w_pcnt)
+// into one sorted top-kp list per query ([q][kp] at the front of w_merged); G lists per block
+// (G x kp <= kMergeMaxKeys: one level for P x kp <= 256 x 64), intermediate levels
+// ping-ponging behind it.
+static int merge_groups(int kp) { return std::min(256, std::max(2, kMergeMaxKeys / kp)); }
+static int merge_lists(hcr_index* ix, int nq, int nqpad, int P, int kp, hipStream_t st,
+                       const uint64_t** out) {
+  static bool lds_set = false;
+  if (!lds_set) {
+    HIPC(hipFuncSetAttribute((const void*)merge_lists_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, kMergeMaxKeys * 8));
+    lds_set = true;
+  }
+  const int G = merge_groups(kp);
+  const int P2 = (P + G - 1) / G;
   const uint64_t* src = ix->w_part.as<const uint64_t>();
-  uint64_t* bufs[2] = {ix->w_merged.as<uint64_t>(),
-                       ix->w_merged.as<uint64_t>() + (size_t)nqpad * std::max(P2, 1) * kp};
+  const int* cnt = ix->w_pcnt.as<const int>();
+  uint64_t* final_dst = ix->w_merged.as<uint64_t>();
+  uint64_t* bufs[2] = {final_dst + (size_t)nqpad * kp, final_dst + (size_t)nqpad * kp * (1 + P2)};
+  int* cbufs[2] = {ix->w_mcnt.as<int>(), ix->w_mcnt.as<int>() + (size_t)nqpad * P2};
   int which = 0, pin = P;
   while (true) {
     const int pout = (pin + G - 1) / G;
     const int M = next_pow2(std::min(G, pin) * kp);
-    uint64_t* dst = bufs[which];
-    hipLaunchKernelGGL(merge_partials_kernel, dim3(nq, pout), dim3(256), (size_t)M * 8, st,
-                       src, pin, G, kp, M, dst);
+    uint64_t* dst = pout == 1 ? final_dst : bufs[which];
+    int* dcnt = pout == 1 ? nullptr : cbufs[which];
+    hipLaunchKernelGGL(merge_lists_kernel, dim3(nq, pout), dim3(256), (size_t)M * 8, st, src, cnt,
+                       pin, G, kp, dst, dcnt);
     HIPC(hipGetLastError());
-    src = dst;
-    which ^= 1;
     if (pout == 1) break;
+    src = dst;
+    cnt = dcnt;
+    which ^= 1;
     pin = pout;
   }
-  *out = src;
+  *out = final_dst;
   return HCR_OK;
+}
+
+// workspace keys of merge_lists: the final [nqpad][kp] list + two ping-pong levels
+static size_t merge_workspace_keys(int nqpad, int P, int kp) {
+  const int G = merge_groups(kp);
+  const size_t P2 = (size_t)((P + G - 1) / G);
+  return (size_t)nqpad * kp * (1 + (P2 > 1 ? 2 * P2 : 0));
 }
 
 // One pipeline pass over nq (<= kQueryChunk) device queries at candidate depth kp.
@@ -659,10 +701,12 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
-  const int nqpad = (int)round_up(nq, tq);
-  const int nqb = nqpad / tq;
+  const bool qs = ver == 3 && c3.qs;
+  // QS batches are padded to 256 queries for their MAXONLY pre-pass on the 256 x 256 kernel
+  const int nqpad = (int)round_up(nq, qs ? 256 : tq);
+  const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
-  const int cap = next_pow2(kp + tr);
+  const int cap = qs ? qs_cap(kp) : next_pow2(kp + tr);
   const int wg_target = ver == 1 ? 512 : 256;
   int P = std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
@@ -676,24 +720,17 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_taug.ensure((size_t)nqpad * 4));
   CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8));
   CHECK(ix->w_part.ensure((size_t)nqpad * P * kp * 8));
-  const int G = std::max(2, kMergeMaxKeys / kp);            // partitions merged per block
-  const int P2 = (P + G - 1) / G;
-  CHECK(ix->w_merged.ensure((size_t)nqpad * std::max(P2, 1) * kp * 8 * 2));
+  CHECK(ix->w_pcnt.ensure((size_t)nqpad * P * 4));
+  CHECK(ix->w_merged.ensure(merge_workspace_keys(nqpad, P, kp) * 8));
+  CHECK(ix->w_mcnt.ensure((size_t)nqpad * ((P + merge_groups(kp) - 1) / merge_groups(kp)) * 4 * 2));
   CHECK(ix->w_unc.ensure((size_t)nqpad * 4));
   CHECK(ix->w_cnt.ensure(16));
   CHECK(ix->w_tauest.ensure((size_t)nqpad * 4));
   CHECK(ix->w_sk.ensure((size_t)nqpad * 8));
-
-  HIPC(hipMemsetAsync(ix->w_qhat.p, 0, (size_t)nqpad * ix->ld * tms, st));
-  HIPC(hipMemsetAsync(ix->w_taug.p, 0, (size_t)nqpad * 4, st));
-  // Padded query columns (q^ = 0, every score 0) get the bound ord32(+inf): with bound 0 they
-  // passed the epilogue's tile test on every tile and sent their waves down the exact path
-  // (r01g: B = 1 on the 256 x 16 tiles slower than B = 16).  Nothing reads their lists.
-  if (nqpad > nq)
-    HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ix->w_taug.as<uint32_t>() + nq),
-                           (int)0xFF800000u, (size_t)(nqpad - nq), st));
-  HIPC(hipMemsetAsync(ix->w_cnt.p, 0, 16, st));
-  HIPC(hipMemsetAsync(ix->w_tauest.p, 0, (size_t)nqpad * 4, st));   // 0 = no estimated bound
+  // (the per-query state -- q^ padding, tau_g, tau_est, the uncertified counter -- is reset
+  // by prep_queries_kernel over the padded batch.  Padded query columns
+  // (q^ = 0, every score 0) get the bound ord32(+inf): with bound 0 they passed the epilogue's
+  // tile test on every tile and sent their waves down the exact path (r01g).)
 
   // rigorous accumulation bound: gamma_{ld+1} + 4u (u = 2^-24)
   const double u = std::ldexp(1.0, -24);
@@ -720,19 +757,22 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double rho = ix->rho_host;
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
-  const bool unit = ver == 3 && c3.rt == 256 && c3.qt == 256 && ix->unit_dev_host <= kUnitDevMax;
+  const bool wide = ver == 3 && c3.rt == 256 && c3.qt == 256;   // v4
+  const bool unit = (wide || qs) && ix->unit_dev_host <= kUnitDevMax;
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
 
-  const unsigned gq = (unsigned)((nq + 3) / 4);
+  const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)
-    hipLaunchKernelGGL((prep_queries_kernel<_Float16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
-                       ix->ld, ix->w_qhat.as<_Float16>(), ix->w_qnorm.as<double>(),
-                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev);
+    hipLaunchKernelGGL((prep_queries_kernel<_Float16>), dim3(gq), dim3(256), 0, st, d_q, nq, nqpad,
+                       ix->dim, ix->ld, ix->w_qhat.as<_Float16>(), ix->w_qnorm.as<double>(),
+                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev, ix->w_taug.as<uint32_t>(),
+                       ix->w_tauest.as<uint32_t>(), ix->w_cnt.as<int>());
   else
-    hipLaunchKernelGGL((prep_queries_kernel<__bf16>), dim3(gq), dim3(256), 0, st, d_q, nq, ix->dim,
-                       ix->ld, ix->w_qhat.as<__bf16>(), ix->w_qnorm.as<double>(),
-                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev);
+    hipLaunchKernelGGL((prep_queries_kernel<__bf16>), dim3(gq), dim3(256), 0, st, d_q, nq, nqpad,
+                       ix->dim, ix->ld, ix->w_qhat.as<__bf16>(), ix->w_qnorm.as<double>(),
+                       ix->w_eps.as<double>(), rho, gamma_u, unit_dev, ix->w_taug.as<uint32_t>(),
+                       ix->w_tauest.as<uint32_t>(), ix->w_cnt.as<int>());
   HIPC(hipGetLastError());
 
   if (ix->timing) HIPC(hipEventRecord(ix->ev0, st));
@@ -752,13 +792,15 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // Two pre-pass forms: MAXONLY (default for the 256 x 256 kernel: the largest score of
       // every sampled 128-row unit per query, no candidate lists, stride 64) and the top-k'
       // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
-      const bool maxonly = !th.prepass_topk && c3.rt == 256 && c3.qt == 256;
+      const bool maxonly = !th.prepass_topk && (wide || qs);
       int stride = th.sample_stride > 0 ? th.sample_stride
                                         : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;
       if (maxonly) stride = std::max<int>(stride, (int)((2 * ntiles + kMaxUnits - 1) / kMaxUnits));
-      V3Launch a{nqb, 0, (int)((ntiles + stride - 1) / stride), stride, kp, unit};
-      a.P = std::max(1, std::min(a.nvt, (wg_target + nqb - 1) / nqb));
+      // (MAXONLY runs on the 256 x 256 kernel: nqpad / 256 query blocks)
+      const int nqb_pre = maxonly ? nqpad / 256 : nqb;
+      V3Launch a{nqb_pre, 0, (int)((ntiles + stride - 1) / stride), stride, kp, unit};
+      a.P = std::max(1, std::min(a.nvt, (wg_target + nqb_pre - 1) / nqb_pre));
       a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
       int j = kp;
       if (!rigorous_seed && !th.rigorous_seed) {
@@ -780,7 +822,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
         if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
         else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
         const uint64_t* sample_best = nullptr;
-        CHECK(merge_tree(ix, nq, nqpad, a.P, P2, G, kp, st, &sample_best));
+        CHECK(merge_lists(ix, nq, nqpad, a.P, kp, st, &sample_best));
         hipLaunchKernelGGL(seed_tau_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
                            sample_best, nq, kp, ix->w_taug.as<uint32_t>(), j,
                            j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
@@ -795,7 +837,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
-  CHECK(merge_tree(ix, nq, nqpad, P, P2, G, kp, st, &merged_ptr));
+  CHECK(merge_lists(ix, nq, nqpad, P, kp, st, &merged_ptr));
 
   if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);

@@ -1,0 +1,384 @@
+// score_qs.h — K2 "query-stationary" (QS): the fused score + top-k' kernel for the batches
+// between the streaming regime (B <= 16, 256 x 16 tiles) and the MFMA-bound regime (B > 256,
+// v4's 256 x 256 tiles): 17..256 queries, where the corpus stream -- N x D x 2 bytes, once --
+// is the roofline (1M x 384 at B = 256 is HBM-bound, 10M x 768 at B <= 64 too).
+//
+// v3/v4 bring a query tile into LDS with every row tile, so the LDS-DMA fill per flop doubles
+// (256 rows + 256 queries per stage) and the fill -- ~7.5 TB/s for the whole chip, near the HBM
+// rate -- becomes the bound at half the HBM roofline.  Here the queries are
+// loaded ONCE into VGPRs as MFMA B fragments (16 queries x the whole K: K/8 VGPRs), and only
+// the corpus rows stream through the LDS-DMA ring:
+//
+//  * workgroup = 8 waves; wave w owns queries [16 w, 16 w + 16) (QT = 128 queries per
+//    workgroup) and computes all RT rows of every tile for them (16 row blocks of 16x16x32
+//    MFMAs per 32-deep half stage);
+//  * the row tile (RT = 256 rows) is streamed in stages of RT x 64 k (32 KiB: four 1 KiB
+//    LDS-DMA pieces per wave), NST-deep ring, each wave waits for its own pieces then one
+//    barrier per stage (as v3).  The stage is large on purpose: a ring stage costs ~1 us of
+//    wait + barrier whatever its size (r02 measurements: 8 KiB stages streamed 1.9 TB/s);
+//  * the k-step loop over a tile is fully unrolled (KS = ld / 32 is a template parameter) so
+//    the query fragments stay in registers;
+//  * the epilogue needs no block synchronisation: a query belongs to one wave, so its
+//    candidate appends, compactions and final list are that wave's alone (compact_query_inl);
+//    its common case (no row of the tile beats any of the wave's bounds) is a max over the
+//    accumulators -- raw for UNIT, scaled by 4 LDS quads of inverse norms otherwise.
+//
+// Grid: nqb query blocks x P row partitions (XCD-aware as v3).  Same outputs as v3: every
+// query's surviving coarse keys of its partition appended to partials[q] (final_list), tau_g
+// raised.
+#pragma once
+#include <utility>
+
+#include "score_v3.h"
+
+namespace hcr {
+
+// 4 row-block fragments (1 KiB apart) at LDS address sbase + voff, issued with no wait;
+// qs_frag_wait<N> then waits until at most N LDS reads are outstanding (they complete in
+// order) and re-defines the fragments so no use of them is scheduled above the wait.  Inline
+// asm: a compiler-visible LDS read after the ring's LDS-DMA gets a vmcnt(0) (ring drained).
+// The stage base is a wave-uniform SGPR operand so that one VGPR (the lane's offset) serves
+// every stage: per-stage address VGPRs were spilled (r02: 249 VGPRs, a scratch reload and a
+// ring drain per tile).
+template <typename V>
+__device__ __forceinline__ void qs_issue_frags4(uint32_t sbase, uint32_t voff, V (&av)[4]) {
+  uint32_t a;
+  asm volatile(
+      "v_add_u32 %4, %5, %6\n\t"
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(a)
+      : "s"(sbase), "v"(voff)
+      : "memory");
+}
+template <int N, typename V>
+__device__ __forceinline__ void qs_frag_wait(V (&av)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]) : "n"(N) : "memory");
+}
+
+// four of a lane's inverse-norm quads (row blocks m0 .. m0+3: 64 B apart), one wait
+__device__ __forceinline__ void qs_read_inv4(uint32_t a, float4 (&v)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:64\n\t"
+      "ds_read_b128 %2, %4 offset:128\n\t"
+      "ds_read_b128 %3, %4 offset:192\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(a)
+      : "memory");
+}
+
+// the 8 row-mask words of a tile (32 B), one wait
+__device__ __forceinline__ void qs_read_u32x8(uint32_t a, uint32_t (&w)[8]) {
+  uint4 x, y;
+  asm volatile(
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %2 offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x), "=&v"(y)
+      : "v"(a)
+      : "memory");
+  w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+  w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+}
+
+template <int NST, int KS>
+struct QsLayout {
+  static constexpr int RT = 256, QT = 128;
+  static constexpr int SPT = KS / 2;                       // stages per tile (64-deep stages)
+  static constexpr int STAGE = RT * 128;                   // 32 KiB: two 32-deep halves
+  // tile slots of inverse norms / bounds / mask words: a tile's slot must outlive the NST-1
+  // stages of look-ahead, (NIS - 1) * SPT > NST - 1
+  static constexpr int NIS = (NST - 1) / SPT + 2;
+  static constexpr int INV = NST * STAGE;                  // NIS x RT floats
+  static constexpr int INV_SLOT = 1024;
+  static constexpr int TG = INV + NIS * INV_SLOT;          // NIS x QT u32 global bounds
+  static constexpr int TG_SLOT = QT * 4;
+  static constexpr int MSK = TG + NIS * TG_SLOT;           // NIS x 32 B of row-mask words
+  static constexpr int TAU = MSK + NIS * 64;               // u64 tau_key[QT]
+  static constexpr int CNT = TAU + QT * 8;                 // int cnt[QT]
+  static constexpr int TOTAL = CNT + QT * 4;
+  static_assert(KS % 2 == 0, "64-deep stages");
+  static_assert(TOTAL <= 160 * 1024, "LDS budget");
+};
+
+// UNIT: the coarse score is the raw dot product (L2-normalised corpora, as score_v4.h UNIT;
+// the host widens the certificate by the corpus' norm deviation).
+template <typename TM, int CAP, int KS, bool UNIT, int NST = 4>
+__global__ void __launch_bounds__(V3_NT, 1)
+score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
+                     const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
+                     const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
+                     uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
+  using L = QsLayout<NST, KS>;
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  constexpr int RT = L::RT, QT = L::QT, MT = RT / 16, D = NST - 1, SPT = L::SPT;
+  static_assert(CAP >= 2 * RT, "candidate buffer must hold a tile's appends after a compaction");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
+  int* cnt = reinterpret_cast<int*>(lds + L::CNT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int qb = g % nqb, p = g / nqb;
+  const int t0 = (int)((int64_t)p * ntiles / P);
+  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
+  const int qbase = qb * QT;
+  uint64_t* wbuf = buf + (size_t)b * QT * CAP;
+  const int wq0 = wave * 16;                      // this wave's first query (block-local)
+  const int qlane = wq0 + (lane & 15);            // the query of this lane's accumulators
+
+  // each wave initialises and owns its queries' state (no block barrier needed for it)
+  if (lane < 16) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
+
+  if (t0 >= t1) {              // an empty partition: empty lists
+    if (lane < 16) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
+    return;
+  }
+
+  // query fragments: lane l holds q^[wq0 + (l & 15)][ks*32 + 8*(l >> 4) .. +8)
+  V qf[KS];
+  {
+    const TM* src = qhat + (size_t)(qbase + qlane) * ld + (lane >> 4) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
+  }
+
+  // DMA: a stage is RT rows x 64 k as two 32-deep halves of the v3 image (16 KiB each, 16 x
+  // 1 KiB pieces of 16 rows x 64 B); wave w issues pieces w, w+8, w+16, w+24
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
+  const int ldb = ld * 2;
+  const int voff = drow * ldb + dchunk * 16;
+  const char* rows_b = reinterpret_cast<const char*>(rows);
+  const __amdgpu_buffer_rsrc_t inv_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(inv_norm), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t tg_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(tau_g + qbase), (short)0, QT * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t msk_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(mask), (short)0, 0x7FFFFFFF, 0x00020000);
+  // tile-start pieces: inverse norms (not read by the UNIT kernel), bounds, mask words
+  const bool extra = (!UNIT && wave == 7) || wave == 6 || (wave == 5 && mask);
+
+  const int nsteps = (t1 - t0) * SPT;
+  // Issue virtual tile vt's stage SP2 into ring slot `slot`.  Every wave issues its four row
+  // pieces; at a tile's first stage waves 7 / 6 / 5 also issue the tile's inverse norms, query
+  // bounds and mask words (SP2 is a compile-time constant, so is that choice).  The per-lane
+  // offsets are re-derived from `lane` here rather than kept live across the loop.
+  auto issue_stage = [&](auto sp2_c, int vt_, int slot_) __attribute__((always_inline)) {
+    constexpr int SP2 = decltype(sp2_c)::value;
+    const int vt = __builtin_amdgcn_readfirstlane(vt_);
+    const int slot = __builtin_amdgcn_readfirstlane(slot_);
+    const int tile = vt * tstride;
+    char* sa = lds + slot * L::STAGE;
+    const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        uniform_ptr(rows_b + (size_t)tile * RT * ldb), (short)0, RT * ldb, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave + 8 * i;            // piece: half j / 16, rows (j % 16) * 16 ..
+      dma16(a_rsrc, sa + j * 1024, voff, (j % 16) * 16 * ldb + (2 * SP2 + j / 16) * (V3_BK * 2));
+    }
+    if constexpr (SP2 == 0) {
+      const int is = vt % L::NIS;
+      int l16;
+      asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(l16) : "v"(lane));
+      if (!UNIT && wave == 7)                // RT inverse norms (1 KiB)
+        dma16(inv_rsrc, lds + L::INV + is * L::INV_SLOT, l16, tile * (RT * 4));
+      if (wave == 6 && lane < QT / 4)
+        dma16(tg_rsrc, lds + L::TG + is * L::TG_SLOT, l16, 0);
+      if (wave == 5 && mask && lane < RT / 32)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            msk_rsrc, (__attribute__((address_space(3))) void*)(lds + L::MSK + is * 64),
+            4, l16 >> 2, tile * (RT / 8), 0, 0);
+    }
+  };
+  // prologue: the first D stages (global stage i = tile t0 + i / SPT, stage i % SPT)
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    ((I < nsteps ? issue_stage(std::integral_constant<int, I % SPT>{}, t0 + I / SPT, I % NST)
+                 : void()), ...);
+  }(std::make_integer_sequence<int, D>{});
+
+  const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
+  const uint32_t lds0 = lds_addr(lds);
+
+  floatx4 acc[MT];
+  bool need = false;                           // some query's buffer must be compacted
+  int s = 0;                                   // global stage index
+  for (int vt = t0; vt < t1; ++vt) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto step = [&](auto sp_c) __attribute__((always_inline)) {
+      constexpr int SP = decltype(sp_c)::value;
+      // stage s landed: this wave's pieces of it.  In steady state the D-1 later stages stay
+      // in flight: 4 pieces each, +1 on waves 5-7 for a tile-start stage among them (a
+      // compile-time count: tile starts are the stages with SP + j == 0 mod SPT); the
+      // stream's last stages wait for everything (nothing left to overlap).
+      constexpr int STARTS = [] {
+        int c = 0;
+        for (int j = 1; j < D; ++j) c += ((SP + j) % SPT == 0) ? 1 : 0;
+        return c;
+      }();
+      if (s + D - 1 < nsteps) {
+        if (extra && STARTS) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1) + STARTS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      v3_barrier();                      // everyone's pieces; everyone done with stage s-1's slot
+      if (s + D < nsteps)
+        issue_stage(std::integral_constant<int, (SP + D) % SPT>{}, vt + (SP + D) / SPT, (s + D) % NST);
+      const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)(lds0 + (uint32_t)((s % NST) * L::STAGE)));
+      // 8 groups of 4 row blocks (2 halves x 4), group j+1's reads in flight under group j's MFMAs
+      V av[2][4];
+      qs_issue_frags4<V>(st, offA, av[0]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int h = j >> 2, g4 = j & 3;
+        if (j < 7) {
+          qs_issue_frags4<V>(st + (uint32_t)(((j + 1) >> 2) * (RT * 64) + ((j + 1) & 3) * 4096), offA,
+                             av[(j + 1) & 1]);
+          qs_frag_wait<4>(av[j & 1]);
+        } else {
+          qs_frag_wait<0>(av[j & 1]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[g4 * 4 + i] = Op::run(av[j & 1][i], qf[2 * SP + h], acc[g4 * 4 + i]);
+      }
+      ++s;
+    };
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (step(std::integral_constant<int, I>{}), ...);
+    }(std::make_integer_sequence<int, SPT>{});
+
+    // ---- epilogue of tile vt (this wave's 16 queries only; no block synchronisation) ----
+    // the lane id through an opaque move: per-row constants derived from it are otherwise
+    // hoisted out of the tile loop as 64 loop-invariant VGPRs (and spilled)
+    int le;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
+    const int lq = le >> 4;
+    const int64_t row0 = (int64_t)vt * tstride * RT;
+    // rows of the tile inside the corpus (row ids fit 32 bits: the coarse keys carry them so)
+    const int nlive = (int)__builtin_amdgcn_readfirstlane(
+        (int)(n_rows - row0 < (int64_t)RT ? n_rows - row0 : (int64_t)RT));
+    const uint32_t row0u = (uint32_t)row0;
+    const int is = vt % L::NIS;
+    const char* invl = lds + L::INV + is * L::INV_SLOT + lq * 16;
+    const char* mskl = lds + L::MSK + is * 64;
+    const uint64_t tk = v3_lds_u64(tau_key + qlane);
+    const float thr =
+        fmaxf(tk ? key_score(tk) : -INFINITY, unord32(v3_lds_u32(lds + L::TG + is * L::TG_SLOT + qlane * 4)));
+    // scores of row block m: the accumulators scaled by the rows' inverse norms (1 for UNIT),
+    // NaN for rows past the corpus end or masked out (they never pass a >= test).  The
+    // inverse norms come 4 row blocks at a time (qs_read_inv4), the 8 mask words at once.
+    const bool live = !mask && nlive == RT;   // every row of the tile counts
+    uint32_t mw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mw[i] = 0xFFFFFFFFu;
+    if (mask) qs_read_u32x8(lds_addr(mskl), mw);
+    auto checked4 = [&](int m4, float (&iv)[4][4]) __attribute__((always_inline)) {
+      float4 v[4];
+      if constexpr (UNIT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+      } else {
+        qs_read_inv4(lds_addr(invl + m4 * 64), v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = (m4 + i) * 16 + lq * 4;
+        const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (rl + r < nlive) && ((mw[(m4 + i) >> 1] >> ((rl + r) & 31)) & 1u);
+          iv[i][r] = ok ? vv[r] : __builtin_nanf("");
+        }
+      }
+    };
+    float mx = -INFINITY;
+    if (live) {
+      if constexpr (UNIT) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m][r]);
+      } else {
+#pragma unroll
+        for (int m4 = 0; m4 < MT; m4 += 4) {
+          float4 iv[4];
+          qs_read_inv4(lds_addr(invl + m4 * 64), iv);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            mx = fmaxf(mx, fmaxf(fmaxf(acc[m4 + i][0] * iv[i].x, acc[m4 + i][1] * iv[i].y),
+                                 fmaxf(acc[m4 + i][2] * iv[i].z, acc[m4 + i][3] * iv[i].w)));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int m4 = 0; m4 < MT; m4 += 4) {
+        float iv[4][4];
+        checked4(m4, iv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m4 + i][r] * iv[i][r]);
+      }
+    }
+    const bool hit = mx >= thr;
+    if (__any(hit)) {
+      // a row is appended when its key beats the query's local k'-th key (same scores as the
+      // max above: x * 1 == x, and the checked path equals the plain one on live rows; unrolled:
+      // a run-time index into acc would put the accumulators in scratch)
+#pragma unroll
+      for (int m4 = 0; m4 < MT; m4 += 4) {
+        float iv[4][4];
+        checked4(m4, iv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sc = acc[m4 + i][r] * iv[i][r];
+            if (hit && sc >= thr) {
+              const uint32_t rowl = row0u + (uint32_t)((m4 + i) * 16 + lq * 4 + r);
+              const uint64_t key = make_key(sc, rowl);
+              if (key > tk) {
+                const int pos = v3_lds_add_rtn(&cnt[qlane], 1);
+                wbuf[(size_t)qlane * CAP + pos] = key;
+                need |= pos + 1 > CAP - RT;
+              }
+            }
+          }
+      }
+      // a query whose buffer cannot take another tile's appends is compacted to its best k'
+      // (rare: drain this wave's stores -- and, in order, its ring pieces -- only then)
+      if (__any(need)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+        for (int ql = wq0; ql < wq0 + 16; ++ql) {
+          if ((int)v3_lds_u32(cnt + ql) > CAP - RT)
+            compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+                               tau_g + qbase + ql, kp, lane, nullptr);
+        }
+        need = false;
+      }
+    }
+  }
+
+  // final: every query's surviving keys (at most k') appended to its region of the partials
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 16, kp, lane, partials, pcnt, P, p);
+}
+
+}  // namespace hcr

@@ -1,0 +1,30 @@
+// score_qs_launch.h — host interface of the query-stationary score kernel (score_qs.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+struct QsArgs {
+  const void* rows;          // corpus rows, storage dtype (f16 / bf16), [n + slack][ld]
+  int ld;
+  int64_t n_rows;
+  const float* inv32;
+  const uint32_t* mask;      // row bitmask or nullptr
+  const void* qhat;          // unit queries, MFMA dtype, [nqb * 128][ld]
+  int nqb, P, ntiles, tstride;
+  uint64_t* buf;             // [nqb * P][QT][cap] candidate buffers
+  uint32_t* tau_g;
+  uint64_t* partials;        // [q][P x kp] append regions (final_list)
+  int* pcnt;                 // [q] append counters
+  int kp;
+  int cap;                   // qs_cap(kp)
+  bool unit;                 // raw dot products as coarse scores (L2-normalised corpus)
+};
+
+// True when a kernel is instantiated for this row stride (128 queries per workgroup).
+bool qs_supported(int ld);
+// Candidate buffer slots per query for k'.
+int qs_cap(int kp);
+// Launch on `st`; HCR_OK or an error code (hcr_last_error()).
+int launch_qs(int dtype, const QsArgs& a, hipStream_t st);
+
+constexpr int kQsRowTile = 256;

@@ -1,8 +1,8 @@
 // score_v3.h — K2 v3: fused score + top-k' with a deep LDS-DMA ring.
 //
-// Same contract as score_topk224_kernel (topk_kernels.h): every workgroup scores a row
+// Same contract as score_topk_kernel (topk_kernels.h): every workgroup scores a row
 // partition against one query block, keeps each query's best k' coarse keys in its
-// candidate buffer and writes them to partials[q][p][0..k').  What changes is the memory
+// candidate buffer and appends them to partials[q] (final_list).  What changes is the memory
 // pipeline, after the r01 profile of v2 (profiles/r01/pmc_summary.txt: 28 % MFMA busy, waves
 // parked 50 % of their cycles in s_waitcnt / barrier, i.e. latency-bound on a 2-deep ring):
 //
@@ -51,7 +51,7 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int kp) {
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
   // ntiles counts VIRTUAL tiles v; virtual tile v is row tile v * tstride (tstride > 1: the
   // sampling pre-pass over every tstride-th tile).  Ring slots and flag parity follow v.
   static_assert(WM * WN == V3_NT / 64, "8 waves");
@@ -86,11 +86,8 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   for (int i = tid; i < QT; i += V3_NT) { tau_key[i] = 0ull; cnt[i] = 0; }
   if (tid == 0) { flag[0] = 0; flag[1] = 0; }
 
-  if (t0 >= t1) {
-    for (int i = tid; i < QT * kp; i += V3_NT) {
-      const int ql = i / kp, j = i - ql * kp;
-      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
-    }
+  if (t0 >= t1) {              // an empty partition: empty lists
+    for (int i = tid; i < QT; i += V3_NT) pcnt[(size_t)(qbase + i) * P + p] = 0;
     return;
   }
 
@@ -282,18 +279,10 @@ score_topk_v3_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
     if (++ks == ksteps) { ks = 0; ++tile; }
   }
 
-  // final: every query's best kp keys -> partials[q][p][0..kp).  All waves' appends first.
+  // final: every query's surviving keys (at most k') appended to its region of the partials.
+  // All waves' appends first.
   __syncthreads();
-  for (int ql = wave; ql < QT; ql += V3_NT / 64) {
-    uint64_t* out = partials + ((size_t)(qbase + ql) * P + p) * kp;
-    const int c = cnt[ql];
-    if (c <= kp) {             // the list already fits: copy (the merge sorts), zero the rest
-      for (int i = lane; i < kp; i += 64) out[i] = i < c ? wbuf[(size_t)ql * CAP + i] : 0ull;
-      continue;
-    }
-    compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
-                           lane, out);
-  }
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wave, V3_NT / 64, QT, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

@@ -82,7 +82,7 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int kp) {
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
   using L = V4Layout<NST>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
@@ -111,12 +111,9 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
   for (int i = tid; i < QT; i += V3_NT) { tau_key[i] = 0ull; cnt[i] = 0; }
   if (tid == 0) { flag[0] = 0; flag[1] = 0; }
 
-  if (t0 >= t1) {
-    if constexpr (MAXONLY) return;
-    for (int i = tid; i < QT * kp; i += V3_NT) {
-      const int ql = i / kp, j = i - ql * kp;
-      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
-    }
+  if (t0 >= t1) {              // an empty partition: empty lists
+    if constexpr (!MAXONLY)
+      for (int i = tid; i < QT; i += V3_NT) pcnt[(size_t)(qbase + i) * P + p] = 0;
     return;
   }
 
@@ -352,16 +349,7 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
 
   if constexpr (MAXONLY) return;
   __syncthreads();
-  for (int ql = wave; ql < QT; ql += V3_NT / 64) {
-    uint64_t* out = partials + ((size_t)(qbase + ql) * P + p) * kp;
-    const int c = cnt[ql];
-    if (c <= kp) {             // the list already fits: copy (the merge sorts), zero the rest
-      for (int i = lane; i < kp; i += 64) out[i] = i < c ? wbuf[(size_t)ql * CAP + i] : 0ull;
-      continue;
-    }
-    compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
-                           lane, out);
-  }
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wave, V3_NT / 64, QT, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

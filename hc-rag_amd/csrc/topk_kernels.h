@@ -7,7 +7,7 @@
 //                            rigorous per-query bound eps_q >= |coarse - exact|.
 //   K2 score_topk_kernel     fused MFMA GEMM (corpus tile x query block) + per-query top-k'
 //                            epilogue: never materialises the B x N score matrix.
-//   K3 merge_partials_kernel per query, P partition lists of k' keys -> global top-k' keys.
+//   K3 merge_lists_kernel    per query, the partitions' surviving keys -> global top-k' keys.
 //   K4 rescore_kernel        fp64 exact cosine of the k' candidates, (score desc, id asc)
 //                            sort, certificate  c_k' + eps_q < s_k, top-k + mode + threshold.
 //   K5 merge_shards_kernel   g row-shards' exact top-k lists -> global top-k (multi-GPU).
@@ -84,15 +84,29 @@ ingest_kernel(const TIN* __restrict__ in, int64_t n, int dim, int ld, int normal
 //   eps = ||q^ - q_n|| + rho*||q^|| + gamma_u*||q^||*(1+rho)   
 //         [+ the UNIT-kernel term when unit_dev >= 0]
 //   eps < 0 marks a zero query (all scores exactly 0).
+// It also resets the pass's per-query state over the padded batch (one launch instead of a
+// memset each): tau_g (0; ord32(+inf) for the padding columns, whose scores are all 0 and
+// must never pass an epilogue test), tau_est (0 = no estimated bound) and the pass's
+// uncertified counter.
 // -------------------------------------------------------------------------------------
 template <typename TM>
 __global__ void __launch_bounds__(256)
-prep_queries_kernel(const float* __restrict__ q32, int nq, int dim, int ld, TM* __restrict__ qhat,
-                    double* __restrict__ qnorm, double* __restrict__ eps, double rho,
-                    double gamma_u, double unit_dev) {
+prep_queries_kernel(const float* __restrict__ q32, int nq, int nqpad, int dim, int ld,
+                    TM* __restrict__ qhat, double* __restrict__ qnorm, double* __restrict__ eps,
+                    double rho, double gamma_u, double unit_dev, uint32_t* __restrict__ tau_g,
+                    uint32_t* __restrict__ tau_est, int* __restrict__ ucnt) {
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (q >= nq) return;
+  if (q >= nqpad) return;
+  if (lane == 0) {
+    tau_g[q] = q < nq ? 0u : 0xFF800000u;
+    tau_est[q] = 0u;
+    if (q == 0) { ucnt[0] = 0; ucnt[1] = 0; ucnt[2] = 0; ucnt[3] = 0; }
+  }
+  if (q >= nq) {
+    for (int d = lane; d < ld; d += 64) qhat[(int64_t)q * ld + d] = (TM)0.0f;
+    return;
+  }
   const float* src = q32 + (int64_t)q * dim;
   double ss = 0.0;
   for (int d = lane; d < dim; d += 64) { const double x = (double)src[d]; ss += x * x; }
@@ -171,6 +185,65 @@ __device__ __forceinline__ void compact_query_inl(uint64_t* __restrict__ qbuf, i
   }
 }
 
+// Final lists of a wave's queries ql = ql0, ql0 + qstep, .. < qend (candidate buffers
+// wbuf[ql][CAP], LDS counts cnt[ql]): the keys whose coarse score reaches the query's CURRENT
+// global bound tau_g go to its list (q, p) of the partials, unsorted (the merge sorts), their
+// number to pcnt[q*P + p].  A key below tau_g is outside the global top-k' (tau_g is a
+// rigorous k'-th coarse score of some workgroup's list, whose k' keys all pass here, or the
+// estimated seed, which the certificate already treats as the bound of the rows it excludes:
+// DESIGN.md §4), so dropping it changes no merged list's top-k'.  Most partitions keep a
+// handful of keys, so the wave sort runs only when more than kp survive, and the merge reads
+// only what was kept.  The next query's keys are loaded while the current one is written (one
+// memory latency per query otherwise: the tail of every score kernel).
+template <int CAP>
+__device__ __forceinline__ void final_lists(uint64_t* __restrict__ wbuf, int* cnt, uint64_t* tau_key,
+                                            uint32_t* tau_g, int qbase, int ql0, int qstep,
+                                            int qend, int kp, int lane, uint64_t* __restrict__ partials,
+                                            int* __restrict__ pcnt, int P, int p) {
+  constexpr int E = CAP / 64;
+  uint64_t v[E];
+  int c = 0;
+  uint32_t tg = 0;
+  auto load = [&](int ql) __attribute__((always_inline)) {
+    c = cnt[ql];
+    tg = __hip_atomic_load(tau_g + qbase + ql, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int idx = e * 64 + lane;
+      v[e] = idx < c ? wbuf[(size_t)ql * CAP + idx] : 0ull;
+    }
+  };
+  if (ql0 < qend) load(ql0);
+  for (int ql = ql0; ql < qend; ql += qstep) {
+    bool keep[E];
+    uint64_t w[E];
+    int n = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      w[e] = v[e];
+      keep[e] = w[e] != 0ull && (uint32_t)(w[e] >> 32) >= tg;
+      n += __popcll(__ballot(keep[e]));
+    }
+    const int qg = qbase + ql;
+    uint64_t* out = partials + ((size_t)qg * P + p) * kp;
+    if (lane == 0) pcnt[(size_t)qg * P + p] = n < kp ? n : kp;
+    if (n > kp) {             // more than k' survive: the wave sort, its best k' written
+      compact_query_inl<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qg, kp, lane, out);
+      if (ql + qstep < qend) load(ql + qstep);
+      continue;
+    }
+    if (ql + qstep < qend) load(ql + qstep);      // in flight under this query's stores
+    int base = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint64_t m = __ballot(keep[e]);
+      const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (keep[e]) out[base + below] = w[e];
+      base += __popcll(m);
+    }
+  }
+}
+
 template <int CAP>
 __device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ qbuf, int* cnt_q,
                                                       uint64_t* tau_key_q, uint32_t* tau_g_q,
@@ -198,7 +271,7 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
                   const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                   const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                   uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                  uint64_t* __restrict__ partials, int kp) {
+                  uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   __shared__ __attribute__((aligned(16))) char lds[LDS_STAGES + BQ * 8 + BQ * 4 + 16];
@@ -221,11 +294,8 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
   for (int i = tid; i < BQ; i += NT) { tau_key[i] = 0ull; cnt[i] = 0; }
   if (tid == 0) *flag = 0;
 
-  if (t0 >= t1) {
-    for (int i = tid; i < BQ * kp; i += NT) {
-      const int ql = i / kp, j = i - ql * kp;
-      partials[((size_t)(qbase + ql) * P + p) * kp + j] = 0ull;
-    }
+  if (t0 >= t1) {              // an empty partition: empty lists
+    for (int i = tid; i < BQ; i += NT) pcnt[(size_t)(qbase + i) * P + p] = 0;
     return;
   }
 
@@ -383,54 +453,152 @@ score_topk_kernel(const TS* __restrict__ rows, int ld, int64_t n_rows, int kstep
     ks = nks;
   }
 
-  // final: every query's best kp keys -> partials[q][p][0..kp)
-  for (int ql = wave; ql < BQ; ql += 4) {
-    compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql], tau_g + qbase + ql, kp,
-                       lane, partials + ((size_t)(qbase + ql) * P + p) * kp);
+  // final: every query's surviving keys (at most k') appended to its region of the partials
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wave, 4, BQ, kp, lane, partials, pcnt, P, p);
+}
+
+// Radix selection by a block of 256 threads over the keys a[0..c), c > kp: moves to the front
+// of a every key whose high word (its coarse score, ord32) is >= that of the kp-th largest key
+// and returns their count (kp, more only with tied scores).  Four passes of 8-bit digits of
+// the high word: LDS histogram, then one wave finds the digit holding the kp-th key.
+__device__ inline int block_select_top_u64(uint64_t* a, int c, int kp, int* hist, int* misc) {
+  const int t = threadIdx.x;
+  uint32_t prefix = 0, pmask = 0;
+  int need = kp;                                   // keys still to take at or below the prefix
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[t] = 0;
+    __syncthreads();
+    for (int e = t; e < c; e += 256) {
+      const uint32_t h = (uint32_t)(a[e] >> 32);
+      if ((h & pmask) == prefix) atomicAdd(&hist[(h >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (t < 64) {
+      int v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = hist[4 * t + j];
+      const int s = v[0] + v[1] + v[2] + v[3];
+      int incl = s;                                // sum over lanes >= t (their bins are higher)
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_down(incl, o);
+        if (t + o < 64) incl += x;
+      }
+      int above = incl - s;
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        if (above < need && above + v[j] >= need) { misc[0] = 4 * t + j; misc[1] = above; }
+        above += v[j];
+      }
+    }
+    __syncthreads();
+    need -= misc[1];
+    prefix |= (uint32_t)misc[0] << shift;
+    pmask |= 255u << shift;
+    __syncthreads();
   }
+  if (t == 0) misc[2] = 0;
+  __syncthreads();
+  for (int e0 = 0; e0 < c; e0 += 256) {            // in-place compaction, chunk by chunk
+    const int e = e0 + t;
+    const uint64_t v = e < c ? a[e] : 0ull;
+    const bool keep = e < c && (uint32_t)(v >> 32) >= prefix;
+    __syncthreads();                               // the chunk is read before any write
+    if (keep) a[atomicAdd(&misc[2], 1)] = v;       // < e0 + 256: never an unread key
+    __syncthreads();
+  }
+  return misc[2];
 }
 
 // -------------------------------------------------------------------------------------
-// K3: merge the P partition lists of one query into its global top-k' (sorted desc).
+// K3: merge the partition survivors of one query into its global top-k' (sorted desc).
 // -------------------------------------------------------------------------------------
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
+// lists: [q][P][kp] slots, list (q, p) holding cnt[q*P + p] keys (a score kernel's final_list
+// or a previous level).  Block (q, grp) gathers lists [grp*G, grp*G + G) (G <= blockDim) into
+// LDS -- a block scan of their counts places them -- and sorts them: with pout == 1 (the last
+// level) it writes the sorted top-kp, zero padded, to out[q*kp ..]; otherwise the top
+// min(count, kp) to list (q, grp) of the next level, [q][pout][kp] with counts cnt_out.
 __global__ void __launch_bounds__(256)
-merge_partials_kernel(const uint64_t* __restrict__ lists, int P, int G, int kp, int M,
-                      uint64_t* __restrict__ out) {
-  // lists: [q][P][kp] sorted-or-not key lists; block (q, grp) merges lists [grp*G, grp*G+G)
-  // into out[q][grp][0..kp) sorted descending.
+merge_lists_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, int P, int G,
+                   int kp, uint64_t* __restrict__ out, int* __restrict__ cnt_out) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm_keys[];
+  __shared__ int s_off[257], s_hist[256], s_misc[4];
   const int q = blockIdx.x, grp = blockIdx.y, pout = gridDim.y;
   const int p0 = grp * G;
   const int np = min(G, P - p0);
-  const uint64_t* src = lists + ((size_t)q * P + p0) * kp;
-  const int tot = np * kp;
-  // Compact the non-empty keys (0 = empty slot) and sort only next_pow2(max(count, kp)) of
-  // them: after a seeded dense pass a query's P lists hold a few hundred keys in P*kp slots
-  // (r01g: 8192-key sorts were 2 x 88 us per search at 1M x 384, B = 256).  Keys are unique
-  // (row id in the low word), so the compaction order does not change the result.
-  __shared__ int s_cnt;
-  if (threadIdx.x == 0) s_cnt = 0;
+  const int t = threadIdx.x;
+  const int c_t = t < np ? min(cnt[(size_t)q * P + p0 + t], kp) : 0;
+  // inclusive scan of the counts (Hillis-Steele over the block)
+  s_off[t + 1] = c_t;
+  if (t == 0) s_off[0] = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (int i0 = 0; i0 < tot; i0 += blockDim.x) {      // uniform trip count: ballot is safe
-    const int i = i0 + threadIdx.x;
-    const uint64_t v = i < tot ? src[i] : 0ull;
-    const uint64_t live = __ballot(v != 0ull);
-    const int wcnt = __popcll(live);
-    int base = 0;
-    if (lane == 0 && wcnt) base = atomicAdd(&s_cnt, wcnt);
-    base = __shfl(base, 0);
-    if (v) sm_keys[base + __popcll(live & ((1ull << lane) - 1ull))] = v;
+  for (int d = 1; d < 256; d <<= 1) {
+    const int x = t + 1 > d ? s_off[t + 1 - d] : 0;
+    __syncthreads();
+    s_off[t + 1] += x;
+    __syncthreads();
+  }
+  const int c = s_off[256];
+  // flat gather: key e of the concatenation comes from the list l with s_off[l] <= e <
+  // s_off[l + 1] (binary search in LDS), so all loads are independent (a wave per list
+  // serialised one memory latency per list: r02m, 68 us at P = 256)
+  const uint64_t* src = lists + ((size_t)q * P + p0) * kp;
+  for (int e = t; e < c; e += blockDim.x) {
+    int lo = 0, hi = np;                                // s_off[lo] <= e < s_off[hi]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid] <= e) lo = mid; else hi = mid;
+    }
+    sm_keys[e] = src[(size_t)lo * kp + (e - s_off[lo])];
   }
   __syncthreads();
-  const int n = s_cnt;
+  // a loose seed leaves several k' keys per query (r02n: ~650 at 1M x 384, k' = 64): select
+  // the top k' by score first, then sort only those
+  const int cs = c > 2 * kp ? block_select_top_u64(sm_keys, c, kp, s_hist, s_misc) : c;
   int m = 1;
-  while (m < n || m < kp) m <<= 1;                    // <= M: n <= tot <= M, kp <= M
-  for (int i = n + threadIdx.x; i < m; i += blockDim.x) sm_keys[i] = 0ull;
+  while (m < cs || m < kp) m <<= 1;                   // <= G * kp (host sizes the LDS)
+  for (int i = cs + t; i < m; i += blockDim.x) sm_keys[i] = 0ull;
   __syncthreads();
   block_sort_desc_u64(sm_keys, m);
+  if (pout == 1) {
+    uint64_t* dst = out + (size_t)q * kp;
+    for (int i = t; i < kp; i += blockDim.x) dst[i] = sm_keys[i];
+    return;
+  }
+  const int take = min(cs, kp);
   uint64_t* dst = out + ((size_t)q * pout + grp) * kp;
-  for (int i = threadIdx.x; i < kp; i += blockDim.x) dst[i] = sm_keys[i];
+  for (int i = t; i < take; i += blockDim.x) dst[i] = sm_keys[i];
+  if (t == 0) cnt_out[(size_t)q * pout + grp] = take;
+}
+#endif
+
+// Eight stored elements of a row (one 16-byte load; two for fp32) as floats.
+template <typename TS>
+__device__ __forceinline__ void load8_f32(const TS* __restrict__ p, float (&x)[8]) {
+  if constexpr (__is_same(TS, float)) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = (float)__builtin_bit_cast(TS, (unsigned short)(w[i] & 0xFFFFu));
+      x[2 * i + 1] = (float)__builtin_bit_cast(TS, (unsigned short)(w[i] >> 16));
+    }
+  }
+}
+
+// The exact-score summation order shared by K4 and K6 (their scores are bit-identical, which
+// the fallback's threshold keys rely on): lane l accumulates dims [8l, 8l + 8), then
+// [8l + 512, ...), in order, in fp64; then the wave sum.  Rows are padded to ld >= dim, a
+// multiple of 64, so the 8-element loads stay inside the row.
+template <typename TQ>
+__device__ __forceinline__ void acc8_f64(double& acc, const TQ* __restrict__ q, int d0, int dim,
+                                         const float (&x)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (d0 + j < dim) acc += (double)q[d0 + j] * (double)x[j];
 }
 
 // -------------------------------------------------------------------------------------
@@ -463,9 +631,9 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
   if (threadIdx.x == 0) s_nvalid = 0;
   __syncthreads();
   const double qn = qnorm[q];
-  // RU candidates per wave at a time, their row gathers in flight together; per candidate
-  // the summation order is the same as one at a time (lane-strided, then the wave sum)
-  constexpr int RU = 8;
+  // RU candidates per wave at a time, their 16-byte row loads in flight together; per
+  // candidate the summation order is acc8_f64's (K6's)
+  constexpr int RU = 16;
   for (int c0 = wave * RU; c0 < kp; c0 += 4 * RU) {
     uint64_t kk[RU];
     const TS* e[RU];
@@ -476,13 +644,12 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
       e[u] = rows + (int64_t)(kk[u] ? key_row(kk[u]) : 0u) * ld;
       acc[u] = 0.0;
     }
-    for (int d = lane; d < dim; d += 64) {
-      const double qv = qd[d];
-      float x[RU];
+    for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+      float x[RU][8];
 #pragma unroll
-      for (int u = 0; u < RU; ++u) x[u] = kk[u] ? (float)e[u][d] : 0.f;
+      for (int u = 0; u < RU; ++u) load8_f32(e[u] + d0, x[u]);
 #pragma unroll
-      for (int u = 0; u < RU; ++u) acc[u] += qv * (double)x[u];
+      for (int u = 0; u < RU; ++u) acc8_f64(acc[u], qd, d0, dim, x[u]);
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
@@ -566,7 +733,11 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
       if (!active[q]) continue;
       const float* qs = q32 + (int64_t)q * dim;
       double acc = 0.0;
-      for (int d = lane; d < dim; d += 64) acc += (double)qs[d] * (double)(float)e[d];
+      for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+        float x[8];
+        load8_f32(e + d0, x);
+        acc8_f64(acc, qs, d0, dim, x);
+      }
       acc = wave_sum_f64(acc);
       if (lane == 0) {
         const uint64_t h = ord64(acc / (qnorm[q] * nr));
@@ -583,6 +754,7 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
   }
 }
 
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void __launch_bounds__(256)
 exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
                     const uint64_t* __restrict__ buf_hi, const uint64_t* __restrict__ buf_lo,
@@ -630,6 +802,7 @@ exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
   __syncthreads();
   if (threadIdx.x == 0) active[q] = 0;
 }
+#endif
 
 // -------------------------------------------------------------------------------------
 // exact fp64 scores of every (query, row) pair (small indexes; isRelevant a1 semantics)
@@ -646,7 +819,11 @@ exact_all_kernel(const float* __restrict__ q32, int dim, const double* __restric
   const float* qs = q32 + (int64_t)q * dim;
   const TS* e = rows + row * ld;
   double acc = 0.0;
-  for (int d = lane; d < dim; d += 64) acc += (double)qs[d] * (double)(float)e[d];
+  for (int d0 = lane * 8; d0 < dim; d0 += 512) {     // K4's order: the same scores bit for bit
+    float x[8];
+    load8_f32(e + d0, x);
+    acc8_f64(acc, qs, d0, dim, x);
+  }
   acc = wave_sum_f64(acc);
   if (lane == 0) {
     double s = acc / (qnorm[q] * norm64[row]);
@@ -658,6 +835,7 @@ exact_all_kernel(const float* __restrict__ q32, int dim, const double* __restric
 // -------------------------------------------------------------------------------------
 // K5: merge g shards' top-k lists ([g][nq][k], exact fp64 scores, -1 = empty).
 // -------------------------------------------------------------------------------------
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void __launch_bounds__(256)
 merge_shards_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g,
                     int64_t nq, int k, int M, double* __restrict__ out_s,
@@ -686,8 +864,10 @@ merge_shards_kernel(const double* __restrict__ s, const int64_t* __restrict__ id
     out_i[q * k + t] = ok ? (int64_t)(~lo[t]) : -1;
   }
 }
+#endif
 
 // gather / scatter helpers for certificate widening
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void gather_rows_f32(const float* __restrict__ src, const int* __restrict__ idx, int n,
                                 int dim, float* __restrict__ dst) {
   const int i = blockIdx.x;
@@ -696,6 +876,8 @@ __global__ void gather_rows_f32(const float* __restrict__ src, const int* __rest
   float* d = dst + (int64_t)i * dim;
   for (int j = threadIdx.x; j < dim; j += blockDim.x) d[j] = s[j];
 }
+#endif
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void scatter_topk(const double* __restrict__ s, const int64_t* __restrict__ ids,
                              const int* __restrict__ idx, int n, int k, double* __restrict__ out_s,
                              int64_t* __restrict__ out_i) {
@@ -706,14 +888,20 @@ __global__ void scatter_topk(const double* __restrict__ s, const int64_t* __rest
     out_i[(int64_t)idx[i] * k + j] = ids[(int64_t)i * k + j];
   }
 }
+#endif
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void iota_ids_kernel(int64_t* __restrict__ ids, int64_t n, int64_t first) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) ids[i] = first + i;
 }
+#endif
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void fill_empty(double* __restrict__ s, int64_t* __restrict__ ids, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) { s[i] = -INFINITY; ids[i] = -1; }
 }
+#endif
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void query_norms_kernel(const float* __restrict__ q32, int nq, int dim,
                                    double* __restrict__ qnorm) {
   const int lane = threadIdx.x & 63;
@@ -724,5 +912,6 @@ __global__ void query_norms_kernel(const float* __restrict__ q32, int nq, int di
   ss = wave_sum_f64(ss);
   if (lane == 0) { double nr = sqrt(ss); qnorm[q] = nr < 10.0 * 2.220446049250313e-16 ? 1.0 : nr; }
 }
+#endif
 
 }  // namespace hcr

@@ -132,14 +132,6 @@ def _bind_hip_runtime():
         p = os.path.join(tl, name)
         if os.path.exists(p):
             ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
-    # torch's RCCL (SONAME librccl.so.1): the multi-device index dlopens that SONAME, so the
-    # process keeps one RCCL on one HIP runtime
-    p = os.path.join(tl, "librccl.so")
-    if os.path.exists(p):
-        try:
-            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
-        except OSError:
-            pass
     _runtime = hip
 
 
