@@ -33,6 +33,19 @@
 
 namespace hcr {
 
+#ifdef HCR_QS_STAMPS
+// Diagnostic build only (Makefile target `stamps`, tools/qs_stamps.py): per wave, the s_memtime
+// cycles spent waiting for a stage (vmcnt + barrier), issuing a stage (DMA + fragment reads +
+// MFMAs), in the tile epilogue, and the tile count.  Never compiled into the product library.
+__device__ unsigned long long hcr_qs_stamps[4096 * 8 * 8];
+#define HCR_QS_STAMP(t)                                                                \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#endif
+
 // 4 row-block fragments (1 KiB apart) at LDS address sbase + voff, issued with no wait;
 // qs_frag_wait<N> then waits until at most N LDS reads are outstanding (they complete in
 // order) and re-defines the fragments so no use of them is scheduled above the wait.  Inline
@@ -211,7 +224,16 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const uint32_t lds0 = lds_addr(lds);
 
   floatx4 acc[MT];
+#ifdef HCR_QS_STAMPS
+  unsigned long long st_wait = 0, st_comp = 0, st_epi = 0, st_fast = 0, st_slow_n = 0, st_t0, st_t1, st_t2;
+#endif
   bool need = false;                           // some query's buffer must be compacted
+  // the lane's query's local k'-th key (only this wave changes it: kept in registers) and its
+  // global bound, re-read every 4th tile: the LDS is the busiest unit of this kernel (every
+  // wave reads every row fragment), an epilogue read waits behind the fragment reads, and a
+  // stale bound is a lower one (more appends, same lists)
+  uint64_t tkr = 0;
+  uint32_t tgr = 0;
   int s = 0;                                   // global stage index
   for (int vt = t0; vt < t1; ++vt) {
 #pragma unroll
@@ -227,6 +249,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         for (int j = 1; j < D; ++j) c += ((SP + j) % SPT == 0) ? 1 : 0;
         return c;
       }();
+#ifdef HCR_QS_STAMPS
+      HCR_QS_STAMP(st_t0);
+#endif
       if (s + D - 1 < nsteps) {
         if (extra && STARTS) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1) + STARTS) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1)) : "memory");
@@ -234,6 +259,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       v3_barrier();                      // everyone's pieces; everyone done with stage s-1's slot
+#ifdef HCR_QS_STAMPS
+      HCR_QS_STAMP(st_t1);
+      st_wait += st_t1 - st_t0;
+#endif
       if (s + D < nsteps)
         issue_stage(std::integral_constant<int, (SP + D) % SPT>{}, vt + (SP + D) / SPT, (s + D) % NST);
       const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -255,6 +284,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         for (int i = 0; i < 4; ++i)
           acc[g4 * 4 + i] = Op::run(av[j & 1][i], qf[2 * SP + h], acc[g4 * 4 + i]);
       }
+#ifdef HCR_QS_STAMPS
+      HCR_QS_STAMP(st_t2);
+      st_comp += st_t2 - st_t1;
+#endif
       ++s;
     };
     [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -262,6 +295,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     }(std::make_integer_sequence<int, SPT>{});
 
     // ---- epilogue of tile vt (this wave's 16 queries only; no block synchronisation) ----
+#ifdef HCR_QS_STAMPS
+    HCR_QS_STAMP(st_t0);
+#endif
     // the lane id through an opaque move: per-row constants derived from it are otherwise
     // hoisted out of the tile loop as 64 loop-invariant VGPRs (and spilled)
     int le;
@@ -275,9 +311,8 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const int is = vt % L::NIS;
     const char* invl = lds + L::INV + is * L::INV_SLOT + lq * 16;
     const char* mskl = lds + L::MSK + is * 64;
-    const uint64_t tk = v3_lds_u64(tau_key + qlane);
-    const float thr =
-        fmaxf(tk ? key_score(tk) : -INFINITY, unord32(v3_lds_u32(lds + L::TG + is * L::TG_SLOT + qlane * 4)));
+    if (((vt - t0) & 3) == 0) tgr = v3_lds_u32(lds + L::TG + is * L::TG_SLOT + qlane * 4);
+    const float thr = fmaxf(tkr ? key_score(tkr) : -INFINITY, unord32(tgr));
     // scores of row block m: the accumulators scaled by the rows' inverse norms (1 for UNIT),
     // NaN for rows past the corpus end or masked out (they never pass a >= test).  The
     // inverse norms come 4 row blocks at a time (qs_read_inv4), the 8 mask words at once.
@@ -335,29 +370,58 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       }
     }
     const bool hit = mx >= thr;
+#ifdef HCR_QS_STAMPS
+    HCR_QS_STAMP(st_t2);
+    st_fast += st_t2 - st_t0;
+    st_slow_n += __any(hit) ? 1 : 0;
+#endif
     if (__any(hit)) {
       // a row is appended when its key beats the query's local k'-th key (same scores as the
-      // max above: x * 1 == x, and the checked path equals the plain one on live rows; unrolled:
-      // a run-time index into acc would put the accumulators in scratch)
+      // max above: x * 1 == x, and the checked path equals the plain one on live rows).
+      // Unrolled (a run-time index into acc would put the accumulators in scratch), with
+      // wave-uniform tests: a tile usually holds one or two rows above a wave's bounds, yet the
+      // path is entered on ~93 % of the tiles (16 queries per wave); per-lane branches over
+      // all 64 elements cost ~8k cycles per tile, one uniform test per element ~5.3k (r02
+      // stamps), one per 4-row block (UNIT, live tile) far less.
+      auto append = [&](float sc, int m, int r) __attribute__((always_inline)) {
+        const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
+        const uint64_t key = make_key(sc, rowl);
+        if (key > tkr) {
+          const int pos = v3_lds_add_rtn(&cnt[qlane], 1);
+          wbuf[(size_t)qlane * CAP + pos] = key;
+          need |= pos + 1 > CAP - RT;
+        }
+      };
+      if (UNIT && live) {
+        // one wave-uniform test per row block (its 4 rows' max, recomputed here: kept from
+        // the max above it costs 16 VGPRs, which the KS = 24 kernel spills), lanes predicated
 #pragma unroll
-      for (int m4 = 0; m4 < MT; m4 += 4) {
-        float iv[4][4];
-        checked4(m4, iv);
+        for (int m = 0; m < MT; ++m) {
+          const bool cg = fmaxf(fmaxf(acc[m][0], acc[m][1]), fmaxf(acc[m][2], acc[m][3])) >= thr;
+          if (__builtin_amdgcn_ballot_w64(cg)) {
+            if (cg) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sc = acc[m4 + i][r] * iv[i][r];
-            if (hit && sc >= thr) {
-              const uint32_t rowl = row0u + (uint32_t)((m4 + i) * 16 + lq * 4 + r);
-              const uint64_t key = make_key(sc, rowl);
-              if (key > tk) {
-                const int pos = v3_lds_add_rtn(&cnt[qlane], 1);
-                wbuf[(size_t)qlane * CAP + pos] = key;
-                need |= pos + 1 > CAP - RT;
-              }
+              for (int r = 0; r < 4; ++r)
+                if (acc[m][r] >= thr) append(acc[m][r], m, r);
             }
           }
+        }
+      } else {
+#pragma unroll
+        for (int m4 = 0; m4 < MT; m4 += 4) {
+          float iv[4][4];
+          checked4(m4, iv);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float sc = acc[m4 + i][r] * iv[i][r];
+              const bool c = sc >= thr;
+              if (__builtin_amdgcn_ballot_w64(c)) {
+                if (c) append(sc, m4 + i, r);
+              }
+            }
+        }
       }
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drain this wave's stores -- and, in order, its ring pieces -- only then)
@@ -371,9 +435,21 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                                tau_g + qbase + ql, kp, lane, nullptr);
         }
         need = false;
+        tkr = v3_lds_u64(tau_key + qlane);
       }
     }
+#ifdef HCR_QS_STAMPS
+    HCR_QS_STAMP(st_t1);
+    st_epi += st_t1 - st_t0;
+#endif
   }
+#ifdef HCR_QS_STAMPS
+  if (lane == 0 && b < 4096) {
+    unsigned long long* o = hcr_qs_stamps + ((size_t)b * 8 + wave) * 8;
+    o[0] = st_wait; o[1] = st_comp; o[2] = st_epi; o[3] = (unsigned long long)(t1 - t0);
+    o[4] = st_fast; o[5] = st_slow_n;
+  }
+#endif
 
   // final: every query's surviving keys (at most k') appended to its region of the partials
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -62,3 +62,9 @@ int launch_qs(int dtype, const QsArgs& a, hipStream_t st) {
   HIPC(hipGetLastError());
   return HCR_OK;
 }
+
+#ifdef HCR_QS_STAMPS
+extern "C" int hcr_debug_qs_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hcr::hcr_qs_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
