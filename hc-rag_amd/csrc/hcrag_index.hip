@@ -452,7 +452,7 @@ static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_c
 //   HCRAG_QS_MAX            largest batch on the query-stationary kernel (0: off)
 struct TestHooks {
   int64_t q64_elems = kQ64WideMaxElems;
-  int qs_max = 128;
+  int qs_max = 256;
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
@@ -475,10 +475,10 @@ static const TestHooks& hooks() {
 struct V3Cfg { int rt, qt, nst; bool qs; };   // qs: query-stationary kernel (score_qs.h)
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
   if (nq <= 16) return {256, 16, 8, false};
-  // 17-128 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
-  // LDS).  r02j (gpurun_out/r02j_*, score ms QS vs v3/v4): 10M x 768 B = 32 2.85 vs 3.69,
-  // B = 128 3.02 vs 4.23, B = 256 (two query blocks) 5.03 vs 4.53; 1M x 384 B = 32 0.215 vs
-  // 0.276, B = 256 0.348 vs 0.313 -> 256 x 256 (v4) from 129 queries.
+  // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
+  // LDS; 129-256 as two 128-query blocks per row partition).  Score ms, QS vs v3/v4
+  // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
+  // vs 4.45, B = 256 4.52 vs 4.59; 1M x 384 B = 32 0.187 vs 0.295, B = 256 0.290 vs 0.331.
   if (nq <= hooks().qs_max && qs_supported(ld)) return {kQsRowTile, 128, 4, true};
   // 17-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
   // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
