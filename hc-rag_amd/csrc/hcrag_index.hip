@@ -473,13 +473,19 @@ static const TestHooks& hooks() {
 }
 
 struct V3Cfg { int rt, qt, nst; bool qs; };   // qs: query-stationary kernel (score_qs.h)
-static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
+static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok) {
   if (nq <= 16) return {256, 16, 8, false};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
   // LDS; 129-256 as two 128-query blocks per row partition).  Score ms, QS vs v3/v4
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
   // vs 4.45, B = 256 4.52 vs 4.59; 1M x 384 B = 32 0.187 vs 0.295, B = 256 0.290 vs 0.331.
-  if (nq <= hooks().qs_max && qs_supported(ld)) return {kQsRowTile, 128, 4, true};
+  if (nq <= hooks().qs_max) {
+    // 129-256 queries with KS <= 12: one 256-query block on 128-row tiles (each row filled
+    // into LDS once instead of once per 128-query block)
+    if (nq > 128 && qs_supported(ld, 2)) return {128, 256, 8, true};
+    // (KS = 24 without the UNIT epilogue spills VGPRs in its tile loop: v3/v4 then)
+    if (qs_supported(ld, 1) && (unit_ok || ld / V3_BK < 24)) return {kQsRowTile, 128, 4, true};
+  }
   // 17-64 queries: 256 x 256 on small corpora (MAXONLY pre-pass), 256 x 64 on large ones.
   // r01g (profiles/r01g/q64_sweeps.jsonl, score kernel ms at B = 48): 1M x 384 0.29 vs 0.36,
   // 1M x 768 0.49 vs 0.52, 2.5M x 768 1.11 vs 1.08, 5M x 768 2.13 vs 1.98, 10M x 768 4.13 vs
@@ -495,6 +501,7 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld) {
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
 static bool v3_fits(const hcr_index* ix, V3Cfg c) {
+  if (c.qs) return true;                   // QS sizes its own slot rings (QsLayout::NIS)
   return (V3_NIS - 1) * (ix->ld / V3_BK) > c.nst - 1;
 }
 
@@ -528,7 +535,8 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
   QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(),
            ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr, ix->w_qhat.p, a.nqb, a.P,
            a.nvt, a.tstride, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit};
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
+           c.qt == 256 ? 2 : 1};
   return launch_qs(ix->dtype, q, st);
 }
 
@@ -698,7 +706,26 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // kernel choice: v3/v4 (deep LDS-DMA ring, tile shape by batch size) for 16-bit rows;
   // v1 (register-staged 128 x 128, converts fp32 rows to bf16 on the way into LDS) for fp32
   // rows and for rows too narrow for the v3 tile-slot rings.
-  const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld);
+  // the corpus' norm statistics (rho, unit deviation): recomputed after an add
+  if (ix->rho_dirty) {
+    unsigned int rho_bits = 0;
+    HIPC(hipStreamSynchronize(ix->stream));
+    HIPC(hipMemcpy(&rho_bits, ix->rho.p, 4, hipMemcpyDeviceToHost));
+    float rho_f;
+    memcpy(&rho_f, &rho_bits, 4);
+    ix->rho_host = (double)rho_f;
+    unsigned long long* ud = reinterpret_cast<unsigned long long*>(ix->rho.as<char>() + 8);
+    HIPC(hipMemsetAsync(ud, 0, 8, ix->stream));
+    hipLaunchKernelGGL(unit_dev_kernel, dim3(1024), dim3(256), 0, ix->stream,
+                       ix->inv32.as<const float>(), ix->n, ud);
+    HIPC(hipGetLastError());
+    unsigned long long ud_bits = 0;
+    HIPC(hipStreamSynchronize(ix->stream));
+    HIPC(hipMemcpy(&ud_bits, ud, 8, hipMemcpyDeviceToHost));
+    memcpy(&ix->unit_dev_host, &ud_bits, 8);
+    ix->rho_dirty = false;
+  }
+  const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
   const bool qs = ver == 3 && c3.qs;
@@ -736,24 +763,6 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double u = std::ldexp(1.0, -24);
   const double nu = (ix->ld + 1) * u;
   const double gamma_u = nu / (1.0 - nu) + 4.0 * u;
-  if (ix->rho_dirty) {
-    unsigned int rho_bits = 0;
-    HIPC(hipStreamSynchronize(ix->stream));
-    HIPC(hipMemcpy(&rho_bits, ix->rho.p, 4, hipMemcpyDeviceToHost));
-    float rho_f;
-    memcpy(&rho_f, &rho_bits, 4);
-    ix->rho_host = (double)rho_f;
-    unsigned long long* ud = reinterpret_cast<unsigned long long*>(ix->rho.as<char>() + 8);
-    HIPC(hipMemsetAsync(ud, 0, 8, ix->stream));
-    hipLaunchKernelGGL(unit_dev_kernel, dim3(1024), dim3(256), 0, ix->stream,
-                       ix->inv32.as<const float>(), ix->n, ud);
-    HIPC(hipGetLastError());
-    unsigned long long ud_bits = 0;
-    HIPC(hipStreamSynchronize(ix->stream));
-    HIPC(hipMemcpy(&ud_bits, ud, 8, hipMemcpyDeviceToHost));
-    memcpy(&ix->unit_dev_host, &ud_bits, 8);
-    ix->rho_dirty = false;
-  }
   const double rho = ix->rho_host;
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
@@ -796,15 +805,18 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       int stride = th.sample_stride > 0 ? th.sample_stride
                                         : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;
-      if (maxonly) stride = std::max<int>(stride, (int)((2 * ntiles + kMaxUnits - 1) / kMaxUnits));
-      // (MAXONLY runs on the 256 x 256 kernel: nqpad / 256 query blocks)
+      // MAXONLY runs on the 256 x 256 kernel: nqpad / 256 query blocks, 256-row tiles (the
+      // dense pass's tiles may be 128 rows: QS with two query blocks per wave)
+      const int tr_pre = maxonly ? 256 : tr;
+      const int64_t ntiles_pre = maxonly ? (ix->n + 255) / 256 : ntiles;
+      if (maxonly) stride = std::max<int>(stride, (int)((2 * ntiles_pre + kMaxUnits - 1) / kMaxUnits));
       const int nqb_pre = maxonly ? nqpad / 256 : nqb;
-      V3Launch a{nqb_pre, 0, (int)((ntiles + stride - 1) / stride), stride, kp, unit};
+      V3Launch a{nqb_pre, 0, (int)((ntiles_pre + stride - 1) / stride), stride, kp, unit};
       a.P = std::max(1, std::min(a.nvt, (wg_target + nqb_pre - 1) / nqb_pre));
       a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
       int j = kp;
       if (!rigorous_seed && !th.rigorous_seed) {
-        const double lam = (double)kp * ((double)a.nvt * tr) / (double)ix->n;
+        const double lam = (double)kp * ((double)a.nvt * tr_pre) / (double)ix->n;
         j = th.seed_rank ? th.seed_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
         j = std::min(kp, std::max(1, j));
       }

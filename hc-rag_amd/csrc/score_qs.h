@@ -9,13 +9,13 @@
 // loaded ONCE into VGPRs as MFMA B fragments (16 queries x the whole K: K/8 VGPRs), and only
 // the corpus rows stream through the LDS-DMA ring:
 //
-//  * workgroup = 8 waves; wave w owns queries [16 w, 16 w + 16) (QT = 128 queries per
-//    workgroup) and computes all RT rows of every tile for them (16 row blocks of 16x16x32
-//    MFMAs per 32-deep half stage);
-//  * the row tile (RT = 256 rows) is streamed in stages of RT x 64 k (32 KiB: four 1 KiB
-//    LDS-DMA pieces per wave), NST-deep ring, each wave waits for its own pieces then one
-//    barrier per stage (as v3).  The stage is large on purpose: a ring stage costs ~1 us of
-//    wait + barrier whatever its size (r02 measurements: 8 KiB stages streamed 1.9 TB/s);
+//  * workgroup = 8 waves; wave w owns NQ blocks of 16 queries (QT = 128 NQ queries per
+//    workgroup) and computes all RT rows of every tile for them (RT/16 row blocks x NQ of
+//    16x16x32 MFMAs per 32-deep half stage): NQ = 1 on 256-row tiles, or NQ = 2 on 128-row
+//    tiles (KS <= 12), where every row is filled into LDS once per 256 queries;
+//  * the row tile is streamed in stages of RT x 64 k (32 or 16 KiB of 1 KiB LDS-DMA pieces),
+//    an NST-deep ring (4 x 32 or 8 x 16 KiB), each wave waits for its own pieces then one
+//    barrier per stage (as v3);
 //  * the k-step loop over a tile is fully unrolled (KS = ld / 32 is a template parameter) so
 //    the query fragments stay in registers;
 //  * the epilogue needs no block synchronisation: a query belongs to one wave, so its
@@ -98,16 +98,16 @@ __device__ __forceinline__ void qs_read_u32x8(uint32_t a, uint32_t (&w)[8]) {
   w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
-template <int NST, int KS>
+template <int NST, int KS, int RT_, int NQ>
 struct QsLayout {
-  static constexpr int RT = 256, QT = 128;
+  static constexpr int RT = RT_, QT = 128 * NQ;
   static constexpr int SPT = KS / 2;                       // stages per tile (64-deep stages)
-  static constexpr int STAGE = RT * 128;                   // 32 KiB: two 32-deep halves
+  static constexpr int STAGE = RT * 128;                   // RT rows x 64 k: two 32-deep halves
   // tile slots of inverse norms / bounds / mask words: a tile's slot must outlive the NST-1
   // stages of look-ahead, (NIS - 1) * SPT > NST - 1
   static constexpr int NIS = (NST - 1) / SPT + 2;
   static constexpr int INV = NST * STAGE;                  // NIS x RT floats
-  static constexpr int INV_SLOT = 1024;
+  static constexpr int INV_SLOT = RT * 4;
   static constexpr int TG = INV + NIS * INV_SLOT;          // NIS x QT u32 global bounds
   static constexpr int TG_SLOT = QT * 4;
   static constexpr int MSK = TG + NIS * TG_SLOT;           // NIS x 32 B of row-mask words
@@ -120,17 +120,24 @@ struct QsLayout {
 
 // UNIT: the coarse score is the raw dot product (L2-normalised corpora, as score_v4.h UNIT;
 // the host widens the certificate by the corpus' norm deviation).
-template <typename TM, int CAP, int KS, bool UNIT, int NST = 4>
+// NQ x 16 queries per wave on RT-row tiles: (1, 256) -- 128 queries per workgroup, any
+// KS <= 24 -- or (2, 128) -- 256 queries per workgroup for KS <= 12 (2 x KS x 4 VGPRs of query
+// fragments): every row is filled into LDS once per 256 queries instead of once per 128.
+template <typename TM, int CAP, int KS, bool UNIT, int NQ = 1, int RT_ = 256,
+          int NST = (RT_ == 256 ? 4 : 8)>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = QsLayout<NST, KS>;
+  using L = QsLayout<NST, KS, RT_, NQ>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int RT = L::RT, QT = L::QT, MT = RT / 16, D = NST - 1, SPT = L::SPT;
+  constexpr int PPH = RT / 16;            // 1 KiB LDS-DMA pieces per 32-deep half of a stage
+  constexpr int PPW = 2 * PPH / 8;        // ... per wave per stage
+  constexpr int NG = MT / 2;              // groups of 4 row blocks per stage (2 halves)
   static_assert(CAP >= 2 * RT, "candidate buffer must hold a tile's appends after a compaction");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -147,27 +154,29 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
   const int qbase = qb * QT;
   uint64_t* wbuf = buf + (size_t)b * QT * CAP;
-  const int wq0 = wave * 16;                      // this wave's first query (block-local)
-  const int qlane = wq0 + (lane & 15);            // the query of this lane's accumulators
+  const int wq0 = wave * 16 * NQ;                 // this wave's first query (block-local)
+  // the query of this lane's accumulators in query block n: wq0 + 16 n + (lane & 15)
+  const int qlane = wq0 + (lane & 15);
 
   // each wave initialises and owns its queries' state (no block barrier needed for it)
-  if (lane < 16) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
+  if (lane < 16 * NQ) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
 
   if (t0 >= t1) {              // an empty partition: empty lists
-    if (lane < 16) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
+    if (lane < 16 * NQ) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
     return;
   }
 
-  // query fragments: lane l holds q^[wq0 + (l & 15)][ks*32 + 8*(l >> 4) .. +8)
-  V qf[KS];
-  {
-    const TM* src = qhat + (size_t)(qbase + qlane) * ld + (lane >> 4) * 8;
+  // query fragments: lane l holds q^[wq0 + 16 n + (l & 15)][ks*32 + 8*(l >> 4) .. +8)
+  V qf[NQ][KS];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
+  for (int n = 0; n < NQ; ++n) {
+    const TM* src = qhat + (size_t)(qbase + qlane + 16 * n) * ld + (lane >> 4) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[n][ks] = *reinterpret_cast<const V*>(src + ks * 32);
   }
 
-  // DMA: a stage is RT rows x 64 k as two 32-deep halves of the v3 image (16 KiB each, 16 x
-  // 1 KiB pieces of 16 rows x 64 B); wave w issues pieces w, w+8, w+16, w+24
+  // DMA: a stage is RT rows x 64 k as two 32-deep halves of the v3 image (PPH 1 KiB pieces of
+  // 16 rows x 64 B each); wave w issues pieces w, w+8, ... (PPW of them)
   const int drow = lane >> 2;
   const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
   const int ldb = ld * 2;
@@ -183,7 +192,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const bool extra = (!UNIT && wave == 7) || wave == 6 || (wave == 5 && mask);
 
   const int nsteps = (t1 - t0) * SPT;
-  // Issue virtual tile vt's stage SP2 into ring slot `slot`.  Every wave issues its four row
+  // Issue virtual tile vt's stage SP2 into ring slot `slot`.  Every wave issues its PPW row
   // pieces; at a tile's first stage waves 7 / 6 / 5 also issue the tile's inverse norms, query
   // bounds and mask words (SP2 is a compile-time constant, so is that choice).  The per-lane
   // offsets are re-derived from `lane` here rather than kept live across the loop.
@@ -196,15 +205,15 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
         uniform_ptr(rows_b + (size_t)tile * RT * ldb), (short)0, RT * ldb, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = wave + 8 * i;            // piece: half j / 16, rows (j % 16) * 16 ..
-      dma16(a_rsrc, sa + j * 1024, voff, (j % 16) * 16 * ldb + (2 * SP2 + j / 16) * (V3_BK * 2));
+    for (int i = 0; i < PPW; ++i) {
+      const int j = wave + 8 * i;            // piece: half j / PPH, rows (j % PPH) * 16 ..
+      dma16(a_rsrc, sa + j * 1024, voff, (j % PPH) * 16 * ldb + (2 * SP2 + j / PPH) * (V3_BK * 2));
     }
     if constexpr (SP2 == 0) {
       const int is = vt % L::NIS;
       int l16;
       asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(l16) : "v"(lane));
-      if (!UNIT && wave == 7)                // RT inverse norms (1 KiB)
+      if (!UNIT && wave == 7 && lane < RT / 4)   // RT inverse norms
         dma16(inv_rsrc, lds + L::INV + is * L::INV_SLOT, l16, tile * (RT * 4));
       if (wave == 6 && lane < QT / 4)
         dma16(tg_rsrc, lds + L::TG + is * L::TG_SLOT, l16, 0);
@@ -223,7 +232,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
   const uint32_t lds0 = lds_addr(lds);
 
-  floatx4 acc[MT];
+  floatx4 acc[MT][NQ];
 #ifdef HCR_QS_STAMPS
   unsigned long long st_wait = 0, st_comp = 0, st_epi = 0, st_fast = 0, st_slow_n = 0, st_t0, st_t1, st_t2;
 #endif
@@ -232,16 +241,20 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   // global bound, re-read every 4th tile: the LDS is the busiest unit of this kernel (every
   // wave reads every row fragment), an epilogue read waits behind the fragment reads, and a
   // stale bound is a lower one (more appends, same lists)
-  uint64_t tkr = 0;
-  uint32_t tgr = 0;
+  uint64_t tkr[NQ];
+  uint32_t tgr[NQ];
+#pragma unroll
+  for (int n = 0; n < NQ; ++n) { tkr[n] = 0; tgr[n] = 0; }
   int s = 0;                                   // global stage index
   for (int vt = t0; vt < t1; ++vt) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
     auto step = [&](auto sp_c) __attribute__((always_inline)) {
       constexpr int SP = decltype(sp_c)::value;
       // stage s landed: this wave's pieces of it.  In steady state the D-1 later stages stay
-      // in flight: 4 pieces each, +1 on waves 5-7 for a tile-start stage among them (a
+      // in flight: PPW pieces each, +1 on waves 5-7 for a tile-start stage among them (a
       // compile-time count: tile starts are the stages with SP + j == 0 mod SPT); the
       // stream's last stages wait for everything (nothing left to overlap).
       constexpr int STARTS = [] {
@@ -253,8 +266,8 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       HCR_QS_STAMP(st_t0);
 #endif
       if (s + D - 1 < nsteps) {
-        if (extra && STARTS) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1) + STARTS) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * (D - 1)) : "memory");
+        if (extra && STARTS) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW * (D - 1) + STARTS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW * (D - 1)) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -267,22 +280,26 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         issue_stage(std::integral_constant<int, (SP + D) % SPT>{}, vt + (SP + D) / SPT, (s + D) % NST);
       const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
           (int)(lds0 + (uint32_t)((s % NST) * L::STAGE)));
-      // 8 groups of 4 row blocks (2 halves x 4), group j+1's reads in flight under group j's MFMAs
+      // NG groups of 4 row blocks (2 halves x MT/4), group j+1's reads in flight under group
+      // j's MFMAs
+      constexpr int GPH = MT / 4;
       V av[2][4];
       qs_issue_frags4<V>(st, offA, av[0]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int h = j >> 2, g4 = j & 3;
-        if (j < 7) {
-          qs_issue_frags4<V>(st + (uint32_t)(((j + 1) >> 2) * (RT * 64) + ((j + 1) & 3) * 4096), offA,
-                             av[(j + 1) & 1]);
+      for (int j = 0; j < NG; ++j) {
+        const int h = j / GPH, g4 = j % GPH;
+        if (j < NG - 1) {
+          qs_issue_frags4<V>(st + (uint32_t)(((j + 1) / GPH) * (RT * 64) + ((j + 1) % GPH) * 4096),
+                             offA, av[(j + 1) & 1]);
           qs_frag_wait<4>(av[j & 1]);
         } else {
           qs_frag_wait<0>(av[j & 1]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[g4 * 4 + i] = Op::run(av[j & 1][i], qf[2 * SP + h], acc[g4 * 4 + i]);
+#pragma unroll
+          for (int n = 0; n < NQ; ++n)
+            acc[g4 * 4 + i][n] = Op::run(av[j & 1][i], qf[n][2 * SP + h], acc[g4 * 4 + i][n]);
       }
 #ifdef HCR_QS_STAMPS
       HCR_QS_STAMP(st_t2);
@@ -311,11 +328,16 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const int is = vt % L::NIS;
     const char* invl = lds + L::INV + is * L::INV_SLOT + lq * 16;
     const char* mskl = lds + L::MSK + is * 64;
-    if (((vt - t0) & 3) == 0) tgr = v3_lds_u32(lds + L::TG + is * L::TG_SLOT + qlane * 4);
-    const float thr = fmaxf(tkr ? key_score(tkr) : -INFINITY, unord32(tgr));
+    if (((vt - t0) & 3) == 0) {
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) tgr[n] = v3_lds_u32(lds + L::TG + is * L::TG_SLOT + (qlane + 16 * n) * 4);
+    }
+    float thr[NQ];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) thr[n] = fmaxf(tkr[n] ? key_score(tkr[n]) : -INFINITY, unord32(tgr[n]));
     // scores of row block m: the accumulators scaled by the rows' inverse norms (1 for UNIT),
     // NaN for rows past the corpus end or masked out (they never pass a >= test).  The
-    // inverse norms come 4 row blocks at a time (qs_read_inv4), the 8 mask words at once.
+    // inverse norms come 4 row blocks at a time (qs_read_inv4), the mask words at once.
     const bool live = !mask && nlive == RT;   // every row of the tile counts
     uint32_t mw[8];
 #pragma unroll
@@ -340,13 +362,17 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         }
       }
     };
-    float mx = -INFINITY;
+    float mx[NQ];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) mx[n] = -INFINITY;
     if (live) {
       if constexpr (UNIT) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m][r]);
+          for (int n = 0; n < NQ; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r]);
       } else {
 #pragma unroll
         for (int m4 = 0; m4 < MT; m4 += 4) {
@@ -354,8 +380,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
           qs_read_inv4(lds_addr(invl + m4 * 64), iv);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            mx = fmaxf(mx, fmaxf(fmaxf(acc[m4 + i][0] * iv[i].x, acc[m4 + i][1] * iv[i].y),
-                                 fmaxf(acc[m4 + i][2] * iv[i].z, acc[m4 + i][3] * iv[i].w)));
+#pragma unroll
+            for (int n = 0; n < NQ; ++n)
+              mx[n] = fmaxf(mx[n], fmaxf(fmaxf(acc[m4 + i][n][0] * iv[i].x, acc[m4 + i][n][1] * iv[i].y),
+                                         fmaxf(acc[m4 + i][n][2] * iv[i].z, acc[m4 + i][n][3] * iv[i].w)));
         }
       }
     } else {
@@ -366,61 +394,71 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, acc[m4 + i][r] * iv[i][r]);
+          for (int n = 0; n < NQ; ++n)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m4 + i][n][r] * iv[i][r]);
       }
     }
-    const bool hit = mx >= thr;
+    bool hit[NQ];
+    bool anyhit = false;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) { hit[n] = mx[n] >= thr[n]; anyhit |= hit[n]; }
 #ifdef HCR_QS_STAMPS
     HCR_QS_STAMP(st_t2);
     st_fast += st_t2 - st_t0;
-    st_slow_n += __any(hit) ? 1 : 0;
+    st_slow_n += __any(anyhit) ? 1 : 0;
 #endif
-    if (__any(hit)) {
+    if (__any(anyhit)) {
       // a row is appended when its key beats the query's local k'-th key (same scores as the
       // max above: x * 1 == x, and the checked path equals the plain one on live rows).
       // Unrolled (a run-time index into acc would put the accumulators in scratch), with
       // wave-uniform tests: a tile usually holds one or two rows above a wave's bounds, yet the
       // path is entered on ~93 % of the tiles (16 queries per wave); per-lane branches over
       // all 64 elements cost ~8k cycles per tile, one uniform test per element ~5.3k (r02
-      // stamps), one per 4-row block (UNIT, live tile) far less.
-      auto append = [&](float sc, int m, int r) __attribute__((always_inline)) {
+      // stamps), one per 4-row block (UNIT, live tile) ~3k.
+      auto append = [&](float sc, int m, int n, int r) __attribute__((always_inline)) {
         const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
         const uint64_t key = make_key(sc, rowl);
-        if (key > tkr) {
-          const int pos = v3_lds_add_rtn(&cnt[qlane], 1);
-          wbuf[(size_t)qlane * CAP + pos] = key;
+        if (key > tkr[n]) {
+          const int ql = qlane + 16 * n;
+          const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+          wbuf[(size_t)ql * CAP + pos] = key;
           need |= pos + 1 > CAP - RT;
         }
       };
-      if (UNIT && live) {
-        // one wave-uniform test per row block (its 4 rows' max, recomputed here: kept from
-        // the max above it costs 16 VGPRs, which the KS = 24 kernel spills), lanes predicated
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const bool cg = fmaxf(fmaxf(acc[m][0], acc[m][1]), fmaxf(acc[m][2], acc[m][3])) >= thr;
-          if (__builtin_amdgcn_ballot_w64(cg)) {
-            if (cg) {
+      for (int n = 0; n < NQ; ++n) {
+        if (!__any(hit[n])) continue;
+        if (UNIT && live) {
+          // one wave-uniform test per row block (its 4 rows' max, recomputed here: kept from
+          // the max above it costs 16 VGPRs, which the KS = 24 kernel spills)
 #pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (acc[m][r] >= thr) append(acc[m][r], m, r);
-            }
-          }
-        }
-      } else {
+          for (int m = 0; m < MT; ++m) {
+            const bool cg = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])) >= thr[n];
+            if (__builtin_amdgcn_ballot_w64(cg)) {
+              if (cg) {
 #pragma unroll
-        for (int m4 = 0; m4 < MT; m4 += 4) {
-          float iv[4][4];
-          checked4(m4, iv);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float sc = acc[m4 + i][r] * iv[i][r];
-              const bool c = sc >= thr;
-              if (__builtin_amdgcn_ballot_w64(c)) {
-                if (c) append(sc, m4 + i, r);
+                for (int r = 0; r < 4; ++r)
+                  if (acc[m][n][r] >= thr[n]) append(acc[m][n][r], m, n, r);
               }
             }
+          }
+        } else {
+#pragma unroll
+          for (int m4 = 0; m4 < MT; m4 += 4) {
+            float iv[4][4];
+            checked4(m4, iv);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float sc = acc[m4 + i][n][r] * iv[i][r];
+                const bool c = sc >= thr[n];
+                if (__builtin_amdgcn_ballot_w64(c)) {
+                  if (c) append(sc, m4 + i, n, r);
+                }
+              }
+          }
         }
       }
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
@@ -429,13 +467,14 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
-        for (int ql = wq0; ql < wq0 + 16; ++ql) {
+        for (int ql = wq0; ql < wq0 + 16 * NQ; ++ql) {
           if ((int)v3_lds_u32(cnt + ql) > CAP - RT)
             compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
                                tau_g + qbase + ql, kp, lane, nullptr);
         }
         need = false;
-        tkr = v3_lds_u64(tau_key + qlane);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) tkr[n] = v3_lds_u64(tau_key + qlane + 16 * n);
       }
     }
 #ifdef HCR_QS_STAMPS
@@ -454,7 +493,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   // final: every query's surviving keys (at most k') appended to its region of the partials
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 16, kp, lane, partials, pcnt, P, p);
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 16 * NQ, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

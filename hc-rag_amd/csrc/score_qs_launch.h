@@ -9,7 +9,7 @@ struct QsArgs {
   int64_t n_rows;
   const float* inv32;
   const uint32_t* mask;      // row bitmask or nullptr
-  const void* qhat;          // unit queries, MFMA dtype, [nqb * 128][ld]
+  const void* qhat;          // unit queries, MFMA dtype, [nqb * 128 * nq_blocks][ld]
   int nqb, P, ntiles, tstride;
   uint64_t* buf;             // [nqb * P][QT][cap] candidate buffers
   uint32_t* tau_g;
@@ -18,13 +18,15 @@ struct QsArgs {
   int kp;
   int cap;                   // qs_cap(kp)
   bool unit;                 // raw dot products as coarse scores (L2-normalised corpus)
+  int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles)
 };
 
-// True when a kernel is instantiated for this row stride (128 queries per workgroup).
-bool qs_supported(int ld);
+// True when a kernel is instantiated for this row stride and query blocks per wave (1: 128
+// queries per workgroup on 256-row tiles; 2: 256 queries on 128-row tiles).
+bool qs_supported(int ld, int nq_blocks);
 // Candidate buffer slots per query for k'.
 int qs_cap(int kp);
 // Launch on `st`; HCR_OK or an error code (hcr_last_error()).
 int launch_qs(int dtype, const QsArgs& a, hipStream_t st);
 
-constexpr int kQsRowTile = 256;
+constexpr int kQsRowTile = 256;       // row tile of the 1-block kernel (128 for 2 blocks)

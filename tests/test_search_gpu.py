@@ -330,6 +330,35 @@ def test_batch_sizes_both_kernels(hc, dtype, B):
         assert ix.last_stats()["uncertified_queries"] == 0
 
 
+@pytest.mark.parametrize("D", [128, 384, 768])
+@pytest.mark.parametrize("B", [17, 200, 256])
+@pytest.mark.parametrize("variant", ["unit", "raw", "masked"])
+def test_query_stationary_kernels(hc, D, B, variant):
+    """The query-stationary kernel (17-256 queries): 1 query block per wave on 256-row tiles
+    (any B at KS = 4..24; B > 128 as two workgroups per partition when D > 384) and 2 blocks
+    per wave on 128-row tiles (B > 128, D <= 384).  Normalised rows (UNIT epilogue), raw rows
+    (inverse norms from LDS; at D = 768 routed to v3/v4), a row mask; N not a multiple of the
+    tile (last tile partly past the corpus end) and large enough for several tiles per
+    workgroup (candidate compactions, the seeded pre-pass)."""
+    rng = np.random.default_rng(D * 1000 + B)
+    N, k = 150000 + 77, 10
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    if variant == "raw":
+        E *= rng.uniform(0.5, 2.0, (N, 1)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[: B // 2] = E[rng.integers(0, N, B // 2)] + 0.2 * rng.standard_normal((B // 2, D)).astype(np.float32)
+    mask = (rng.random(N) < 0.7) if variant == "masked" else None
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=(variant != "raw"))
+        if mask is not None:
+            ix.set_rowmask(mask)
+        R = ix.get_rows()
+        s, i = ix.search(Q, k)
+        es, ei = O.cosine_topk(Q, R, k, rowmask=mask)
+        _check(s, i, es, ei)
+        assert ix.last_stats()["uncertified_queries"] == 0
+
+
 _NARROW = r"""
 import sys, numpy as np
 sys.path[:0] = [sys.argv[1], sys.argv[2]]
