@@ -282,25 +282,34 @@ score_topk_v4_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows, int ks
         }
         if constexpr (MAXONLY) any = false;
         if (__any(any)) {
+          // wave-uniform tests per query block and per 4-row block, lanes predicated inside
+          // (per-lane branches over every element cost ~3x as much: r02 stamps of the QS
+          // kernel's identical path)
 #pragma unroll
           for (int n = 0; n < NQ; ++n) {
-            if (hit[n]) {
-              const int ql = wn * 64 + n * 16 + lr;
+            if (!__any(hit[n])) continue;
+            const int ql = wn * 64 + n * 16 + lr;
 #pragma unroll
-              for (int m = 0; m < MT; ++m)
+            for (int m = 0; m < MT; ++m) {
+              const bool cg = fmaxf(fmaxf(score(m, n, 0), score(m, n, 1)),
+                                    fmaxf(score(m, n, 2), score(m, n, 3))) >= thr[n];
+              if (__builtin_amdgcn_ballot_w64(cg)) {
+                if (cg) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const float sc = score(m, n, r);
-                  if (sc >= thr[n]) {
-                    const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
-                    const uint64_t key = make_key(sc, rowl);
-                    if (key > tkr[n]) {
-                      const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-                      wbuf[(size_t)ql * CAP + pos] = key;
-                      if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
+                  for (int r = 0; r < 4; ++r) {
+                    const float sc = score(m, n, r);
+                    if (sc >= thr[n]) {
+                      const uint32_t rowl = (uint32_t)(row0 + wm * 128 + m * 16 + lq * 4 + r);
+                      const uint64_t key = make_key(sc, rowl);
+                      if (key > tkr[n]) {
+                        const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+                        wbuf[(size_t)ql * CAP + pos] = key;
+                        if (pos + 1 > CAP - RT) v3_lds_store_u32(cur_flag, 1u);
+                      }
                     }
                   }
                 }
+              }
             }
           }
         }
