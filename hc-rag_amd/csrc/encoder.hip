@@ -327,27 +327,6 @@ static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, in
 static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
                                 hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
-  if (S <= 64 && (dh == 32 || dh == 64)) {      // short sequences: lane per query token
-    if (attention_f32_short_lds(S, dh) > 64 * 1024) {
-      static bool set64 = false, set32 = false;
-      bool& set = dh == 64 ? set64 : set32;
-      if (!set) {
-        HIPC(hipFuncSetAttribute(dh == 64 ? (const void*)attention_f32_short_kernel<64>
-                                          : (const void*)attention_f32_short_kernel<32>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        set = true;
-      }
-    }
-    const unsigned grid = (unsigned)(n * ((e->cfg.heads + 3) / 4));
-    if (dh == 64)
-      hipLaunchKernelGGL((attention_f32_short_kernel<64>), dim3(grid), dim3(256), attention_f32_short_lds(S, 64), st,
-                         e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
-    else
-      hipLaunchKernelGGL((attention_f32_short_kernel<32>), dim3(grid), dim3(256), attention_f32_short_lds(S, 32), st,
-                         e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
-    HIPC(hipGetLastError());
-    return HCR_OK;
-  }
   const bool kv_lds = attention_f32_lds(S, dh, true) <= 160 * 1024;
   const size_t lds = attention_f32_lds(S, dh, kv_lds);
   if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);

@@ -507,91 +507,6 @@ attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ 
   }
 }
 
-// Short sequences (S <= 64, the query-embedding regime): one wave per (sequence, head), lane i
-// = query token i with its q row, score row and output row in registers; K and V of the head
-// staged in LDS and read as wave-wide broadcasts.  4 heads per 256-thread block.  Same
-// arithmetic as attention_f32_kernel (fp32 dot products, expf softmax over the unmasked keys,
-// fp32 P.V), but every lane works on its own query instead of a wave walking the queries:
-// r02 profile, bge-base S = 32: 399 us per layer call for the wave-per-query kernel.
-__host__ __device__ inline size_t attention_f32_short_lds(int S, int dh) {
-  return (size_t)4 * (2 * S * dh + 64) * 4;
-}
-template <int DH>
-__global__ void __launch_bounds__(256)
-attention_f32_short_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
-                           int H, int heads, _Float16* __restrict__ ctx) {
-  constexpr int SM = 64;
-  // per wave: K [S][DH], V [S][DH], key mask [S] (dynamic LDS: attention_f32_short_lds)
-  extern __shared__ __attribute__((aligned(16))) float atts_sm[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int hg = (heads + 3) / 4;
-  const int bidx = blockIdx.x / hg, h = (blockIdx.x % hg) * 4 + wave;
-  if (h >= heads) return;                      // (no block barrier below: waves independent)
-  const size_t row0 = (size_t)bidx * S;
-  const int ld3 = 3 * H;
-  float* wsm = atts_sm + (size_t)wave * (2 * S * DH + SM);
-  float (*Ks)[DH] = reinterpret_cast<float (*)[DH]>(wsm);
-  float (*Vs)[DH] = reinterpret_cast<float (*)[DH]>(wsm + S * DH);
-  float* mk = wsm + 2 * S * DH;
-  for (int i = lane; i < S * DH; i += 64) {
-    const int j = i / DH, d = i - j * DH;
-    const float* base = qkv + (row0 + j) * ld3 + h * DH + d;
-    Ks[j][d] = base[H];
-    Vs[j][d] = base[2 * H];
-  }
-  if (lane < S) mk[lane] = mask[row0 + lane] ? 0.f : -INFINITY;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane >= S) return;
-  float q[DH];
-  const float* qrow = qkv + (row0 + lane) * ld3 + h * DH;
-#pragma unroll
-  for (int d = 0; d < DH; d += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(qrow + d);
-    q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
-  }
-  const float sq = sqrtf((float)DH);          // HF: scores / sqrt(head_size)
-  float p[SM];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < SM; ++j) {
-    p[j] = -INFINITY;
-    if (j < S) {
-      float acc = 0.f;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) acc = fmaf(q[d], Ks[j][d], acc);
-      p[j] = acc / sq + mk[j];
-      mx = fmaxf(mx, p[j]);
-    }
-  }
-  float sum = 0.f;
-#pragma unroll
-  for (int j = 0; j < SM; ++j) {
-    if (j < S) {
-      p[j] = (mx == -INFINITY) ? 0.f : expf(p[j] - mx);
-      sum += p[j];
-    }
-  }
-  const float inv = sum > 0.f ? 1.f / sum : 0.f;
-  _Float16* crow = ctx + (row0 + lane) * ld3;
-#pragma unroll
-  for (int d0 = 0; d0 < DH; d0 += 16) {
-    float o[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) o[t] = 0.f;
-#pragma unroll
-    for (int j = 0; j < SM; ++j) {
-      if (j < S) {
-#pragma unroll
-        for (int t = 0; t < 16; ++t) o[t] = fmaf(p[j], Vs[j][d0 + t], o[t]);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 16; ++t) store_act1<_Float16, true>(crow, H, h * DH + d0 + t, o[t] * inv);
-  }
-}
-
 // -------------------------------------------------------------------------------------
 // Pooling + L2 normalise (one block per sequence).
 //   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
