@@ -327,6 +327,25 @@ static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, in
 static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
                                 hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
+  if (S <= 64 && (dh == 32 || dh == 64)) {      // short sequences: f32 MFMA tiles
+    const int nt = (S + 15) / 16;
+    const size_t lds = attention_f32_mfma_lds(nt, dh);
+    const unsigned grid = (unsigned)(n * e->cfg.heads);
+#define HCR_ATT_MFMA(DH_, NT_)                                                                    \
+  hipLaunchKernelGGL((attention_f32_mfma_kernel<DH_, NT_>), dim3(grid), dim3(64), lds, st,        \
+                     e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads,            \
+                     e->ctx.as<_Float16>())
+    if (dh == 64) {
+      switch (nt) { case 1: HCR_ATT_MFMA(64, 1); break; case 2: HCR_ATT_MFMA(64, 2); break;
+                    case 3: HCR_ATT_MFMA(64, 3); break; default: HCR_ATT_MFMA(64, 4); break; }
+    } else {
+      switch (nt) { case 1: HCR_ATT_MFMA(32, 1); break; case 2: HCR_ATT_MFMA(32, 2); break;
+                    case 3: HCR_ATT_MFMA(32, 3); break; default: HCR_ATT_MFMA(32, 4); break; }
+    }
+#undef HCR_ATT_MFMA
+    HIPC(hipGetLastError());
+    return HCR_OK;
+  }
   const bool kv_lds = attention_f32_lds(S, dh, true) <= 160 * 1024;
   const size_t lds = attention_f32_lds(S, dh, kv_lds);
   if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);

@@ -507,6 +507,123 @@ attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ 
   }
 }
 
+// Reference-precision attention for short sequences (S <= 64, the query-embedding regime) on
+// the f32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation; MICROARCH
+// "FP32-input MFMA"): one 64-thread workgroup per (sequence, head); Q, K, V staged in LDS
+// (rows padded to DH + 1 floats: conflict-free column reads); S = Q·Kᵀ / sqrt(DH) + key mask
+// as NT x NT 16x16 tiles, the row softmax across the 16 lanes of a tile row, P through LDS,
+// O = P·V as NT x DH/16 tiles scaled by 1 / row sum.  r02 profile, bge-base S = 32: the
+// wave-per-query kernel (attention_f32_kernel) took 399 us per layer call.
+__host__ __device__ inline size_t attention_f32_mfma_lds(int nt, int dh) {
+  const int s16 = 16 * nt;
+  return ((size_t)3 * s16 * (dh + 1) + (size_t)s16 * (s16 + 1) + s16) * 4;
+}
+template <int DH, int NT>
+__global__ void __launch_bounds__(64)
+attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
+                          int H, int heads, _Float16* __restrict__ ctx) {
+  constexpr int S16 = 16 * NT, LD = DH + 1, LP = S16 + 1;
+  extern __shared__ __attribute__((aligned(16))) float attm_sm[];
+  float* Qs = attm_sm;
+  float* Ks = Qs + S16 * LD;
+  float* Vs = Ks + S16 * LD;
+  float* Ps = Vs + S16 * LD;
+  float* mk = Ps + S16 * LP;
+  const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
+  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  const size_t row0 = (size_t)bidx * S;
+  const int ld3 = 3 * H;
+  // stage Q, K, V (rows >= S zero)
+  for (int e = lane; e < S16 * (DH / 4); e += 64) {
+    const int j = e / (DH / 4), d = (e % (DH / 4)) * 4;
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f), k = q, v = q;
+    if (j < S) {
+      const float* base = qkv + (row0 + j) * ld3 + h * DH + d;
+      q = *reinterpret_cast<const float4*>(base);
+      k = *reinterpret_cast<const float4*>(base + H);
+      v = *reinterpret_cast<const float4*>(base + 2 * H);
+    }
+    float* qd = Qs + j * LD + d;
+    float* kd = Ks + j * LD + d;
+    float* vd = Vs + j * LD + d;
+    qd[0] = q.x; qd[1] = q.y; qd[2] = q.z; qd[3] = q.w;
+    kd[0] = k.x; kd[1] = k.y; kd[2] = k.z; kd[3] = k.w;
+    vd[0] = v.x; vd[1] = v.y; vd[2] = v.z; vd[3] = v.w;
+  }
+  for (int j = lane; j < S16; j += 64) mk[j] = (j < S && mask[row0 + j]) ? 0.f : -INFINITY;
+  __syncthreads();
+  // scores
+  floatx4 c[NT][NT];
+#pragma unroll
+  for (int it = 0; it < NT; ++it)
+#pragma unroll
+    for (int jt = 0; jt < NT; ++jt) c[it][jt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int d0 = 0; d0 < DH; d0 += 4) {
+    float a[NT], b[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a[t] = Qs[(t * 16 + lr) * LD + d0 + lk];
+      b[t] = Ks[(t * 16 + lr) * LD + d0 + lk];
+    }
+#pragma unroll
+    for (int it = 0; it < NT; ++it)
+#pragma unroll
+      for (int jt = 0; jt < NT; ++jt)
+        c[it][jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[it], b[jt], c[it][jt], 0, 0, 0);
+  }
+  // row softmax: row it*16 + 4 lk + r lives in the 16 lanes with this lk (column = jt*16 + lr)
+  const float sq = sqrtf((float)DH);      // HF: scores / sqrt(head_size)
+  float inv[NT][4];
+#pragma unroll
+  for (int it = 0; it < NT; ++it)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int jt = 0; jt < NT; ++jt) {
+        const float v = c[it][jt][r] / sq + mk[jt * 16 + lr];
+        c[it][jt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int jt = 0; jt < NT; ++jt) {
+        const float e = (mx == -INFINITY) ? 0.f : expf(c[it][jt][r] - mx);
+        Ps[(it * 16 + 4 * lk + r) * LP + jt * 16 + lr] = e;
+        sum += e;
+      }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) sum += __shfl_xor(sum, m, 64);
+      inv[it][r] = sum > 0.f ? 1.f / sum : 0.f;
+    }
+  __syncthreads();
+  // O = P.V, per 16-column block of the head
+#pragma unroll
+  for (int dt = 0; dt < DH / 16; ++dt) {
+    floatx4 o[NT];
+#pragma unroll
+    for (int it = 0; it < NT; ++it) o[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j0 = 0; j0 < S16; j0 += 4) {
+      const float b = Vs[(j0 + lk) * LD + dt * 16 + lr];
+#pragma unroll
+      for (int it = 0; it < NT; ++it)
+        o[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ps[(it * 16 + lr) * LP + j0 + lk], b, o[it], 0, 0, 0);
+    }
+#pragma unroll
+    for (int it = 0; it < NT; ++it)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = it * 16 + 4 * lk + r;
+        if (i < S)
+          store_act1<_Float16, true>(ctx + (row0 + i) * ld3, H, h * DH + dt * 16 + lr, o[it][r] * inv[it][r]);
+      }
+  }
+}
+
 // -------------------------------------------------------------------------------------
 // Pooling + L2 normalise (one block per sequence).
 //   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
