@@ -220,17 +220,17 @@ def test_device_api_and_shard_merge(hc):
     _check(out_s.cpu().numpy(), out_i.cpu().numpy(), es, ei, tol=SCORE_TOL_F64)
 
 
-@pytest.mark.parametrize("W", [2, 8])
-def test_rank_shapes_of_the_scaling_bench(hc, W):
+@pytest.mark.parametrize("W,B", [(2, 1024), (8, 1024), (8, 512)])
+def test_rank_shapes_of_the_scaling_bench(hc, W, B):
     """The local search each rank of ``bench.py --gpus W`` runs: nq = W x B gathered queries
-    (8192 at W = 8) over a row shard, through the same hip_local_search / hip_merge callables
+    (8192 at W = 8, B = 1024; 4096 = configs[3]'s global batch at W = 8, B = 512) over a row shard, through the same hip_local_search / hip_merge callables
     ShardedSearch uses; the W shards run one after another on one GPU, the all-to-all is the
     slice [j*B:(j+1)*B] of shard r's result, and the merged lists must equal the unsharded
     oracle exactly."""
     torch = pytest.importorskip("torch")
     from hcrag_amd.distributed import shard_range, hip_local_search, hip_merge
     rng = np.random.default_rng(100 + W)
-    D, N, B, k = 768, 12000, 1024, 32
+    D, N, k = 768, 12000, 32
     E = rng.standard_normal((N, D)).astype(np.float16)
     Q = rng.standard_normal((W * B, D)).astype(np.float32)
     planted = rng.integers(0, N, W * B // 2)
