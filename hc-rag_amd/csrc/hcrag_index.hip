@@ -450,9 +450,11 @@ static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_c
 //   HCRAG_SEED_RANK         force seed rank j (aggressive seeds exercise the re-runs)
 //   HCRAG_PREPASS_TOPK      the top-k' pre-pass form instead of MAXONLY
 //   HCRAG_QS_MAX            largest batch on the query-stationary kernel (0: off)
+//   HCRAG_QW_MIN            smallest batch on the wide query-stationary kernel
 struct TestHooks {
   int64_t q64_elems = kQ64WideMaxElems;
   int qs_max = 256;
+  int qw_min = 257;
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
@@ -461,6 +463,7 @@ static const TestHooks& hooks() {
     TestHooks t;
     if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
     if (const char* e = getenv("HCRAG_QS_MAX")) t.qs_max = atoi(e);
+    if (const char* e = getenv("HCRAG_QW_MIN")) t.qw_min = std::max(1, atoi(e));
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
@@ -472,9 +475,14 @@ static const TestHooks& hooks() {
   return h;
 }
 
-struct V3Cfg { int rt, qt, nst; bool qs; };   // qs: query-stationary kernel (score_qs.h)
-static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok) {
+// qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h)
+struct V3Cfg { int rt, qt, nst; bool qs, qw = false; };
+// qw_ok: a UNIT corpus without a row mask and k' small enough for the QW candidate buffers
+static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok) {
   if (nq <= 16) return {256, 16, 8, false};
+  // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
+  // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
+  if (nq >= hooks().qw_min && unit_ok && qw_ok && qw_supported(ld)) return {qw_rows(ld), kQwQueries, kQwStages, false, true};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
   // LDS; 129-256 as two 128-query blocks per row partition).  Score ms, QS vs v3/v4
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
@@ -501,7 +509,7 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok) {
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
 static bool v3_fits(const hcr_index* ix, V3Cfg c) {
-  if (c.qs) return true;                   // QS sizes its own slot rings (QsLayout::NIS)
+  if (c.qs || c.qw) return true;                  // QS sizes its own slot rings (QsLayout::NIS)
   return (V3_NIS - 1) * (ix->ld / V3_BK) > c.nst - 1;
 }
 
@@ -538,6 +546,13 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
            c.qt == 256 ? 2 : 1};
   return launch_qs(ix->dtype, q, st);
+}
+
+static int launch_qw_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
+  QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
+           a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
+  return launch_qw(ix->dtype, q, st);
 }
 
 template <typename TM, int CAP>
@@ -590,6 +605,7 @@ static int launch_v4_maxonly(hcr_index* ix, V3Launch a, hipStream_t st) {
 template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
   if (c.qs) return launch_qs_ix(ix, c, a, st);              // CAP chosen in score_qs.hip
+  if (c.qw) return launch_qw_ix(ix, a, cap, st);
   switch (cap) {
     case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
     case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
@@ -725,17 +741,19 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     memcpy(&ix->unit_dev_host, &ud_bits, 8);
     ix->rho_dirty = false;
   }
-  const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax);
+  const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
+                          !ix->has_mask && ix->dtype != HCR_F32 && qw_cap(kp, ix->ld) > 0);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
-  const bool qs = ver == 3 && c3.qs;
+  const bool qs = ver == 3 && c3.qs, qw = ver == 3 && c3.qw;
   // QS batches are padded to 256 queries for their MAXONLY pre-pass on the 256 x 256 kernel
   const int nqpad = (int)round_up(nq, qs ? 256 : tq);
   const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
-  const int cap = qs ? qs_cap(kp) : next_pow2(kp + tr);
+  const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : next_pow2(kp + tr);
   const int wg_target = ver == 1 ? 512 : 256;
-  int P = std::max(1, (wg_target + nqb - 1) / nqb);
+  // (QW: one workgroup per CU -- its LDS -- so at most 256 workgroups: one round)
+  int P = qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
   const bool tm_f16 = ix->dtype == HCR_F16;
@@ -767,9 +785,10 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
   const bool wide = ver == 3 && c3.rt == 256 && c3.qt == 256;   // v4
-  const bool unit = (wide || qs) && ix->unit_dev_host <= kUnitDevMax;
+  const bool unit = (wide || qs || qw) && ix->unit_dev_host <= kUnitDevMax;
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
+  if (ix->stats.score_kernel == 0) ix->stats.score_kernel = ver == 1 ? 1 : qw ? 6 : qs ? 5 : wide ? 4 : 3;
 
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)
@@ -801,7 +820,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // Two pre-pass forms: MAXONLY (default for the 256 x 256 kernel: the largest score of
       // every sampled 128-row unit per query, no candidate lists, stride 64) and the top-k'
       // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
-      const bool maxonly = !th.prepass_topk && (wide || qs);
+      const bool maxonly = !th.prepass_topk && (wide || qs || qw);
       int stride = th.sample_stride > 0 ? th.sample_stride
                                         : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;

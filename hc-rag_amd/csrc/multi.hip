@@ -246,6 +246,7 @@ extern "C" int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_
     m->stats.fallback_rounds += st.fallback_rounds;
     m->stats.partitions += st.partitions;
     m->stats.workgroups += st.workgroups;
+    m->stats.score_kernel = std::max(m->stats.score_kernel, st.score_kernel);
   }
   // 2) exchange: every shard's lists to shard 0's device as [g][nq][k]
   hcr_multi_shard& s0 = m->sh[0];

@@ -1,0 +1,271 @@
+// score_qw.h — K2 "QW": query-stationary fused score + top-k' for LARGE batches (> 256
+// queries, the MFMA-bound regime of configs[2]: 10M x 768, B = 1024).
+//
+// Why a third kernel.  v4 (score_v4.h) fills a 256-row and a 256-query tile into LDS for every
+// 32-deep stage: 32 KiB of LDS-DMA per 4.2 MFLOP, i.e. 32 B/clk/CU at the MFMA peak, against
+// a measured LDS-DMA fill ceiling of ~12-16 B/clk/CU (7.6 TB/s chip-wide) -- the
+// main loop is fill-bound at ~40 % of the MFMA peak.  QS (score_qs.h) keeps the queries in
+// VGPRs but only 128 per workgroup at D = 768 (16 per wave), so rows are still filled once per
+// 128 queries.  QW holds 256 queries x the whole K in the workgroup's registers -- 32 queries
+// per wave, 2 x KS fragments each (192 VGPRs at D = 768: three quarters of the CU's register
+// file are query operands) -- and streams only rows: 16 B/clk/CU at the MFMA peak, half of v4.
+//
+//  * a stage is a whole row tile over the full K: SR rows x ld (SR = 32 at D = 768, 64 at
+//    D = 384: 48 KiB), a 3-deep ring (two stages in flight), one barrier per stage;
+//  * the stage's LDS image is the v3 one (1 KiB pieces of 16 rows x 32 k, XOR-swizzled chunks):
+//    piece (rb, ks) at (rb x KS + ks) KiB; each wave DMAs 6 of the 48 pieces plus its 32 global
+//    bounds (a 4-byte-per-lane LDS-DMA: 7 vmcnt-counted ops per wave per stage);
+//  * per stage a wave runs RB x KS x 2 MFMAs (96 at D = 768: 1536 cycles) on 4 independent
+//    accumulator chains (row-block pair x query-block pair), fragment reads two groups ahead;
+//  * the epilogue is per stage (the accumulators of SR rows x 32 queries: 16 VGPRs), a max +
+//    compare against max(local k'-th key, global bound); appends, compactions and the final
+//    lists are the wave's alone (its queries), as in QS.
+//
+// UNIT corpora only (raw dot product = coarse score) and no row mask: other
+// batches run on v4.  Rows of the last tile past n_rows are excluded in its epilogue.
+// Grid: nqb query blocks x P row partitions (XCD-aware as v3/v4), one workgroup per CU (LDS).
+#pragma once
+#include <utility>
+
+#include "score_v3.h"
+
+namespace hcr {
+
+constexpr int QW_QT = 256;      // queries per workgroup (8 waves x 32; kQwQueries on the host)
+constexpr int QW_NST = 3;       // ring stages
+
+// rows per stage for KS 32-deep k-steps: 48 KiB stages (RB = SR / 16 row blocks, even)
+constexpr int qw_sr(int ks) { return ks == 24 ? 32 : ks == 12 ? 64 : 0; }
+
+template <int KS>
+struct QwLayout {
+  static constexpr int SR = qw_sr(KS), RB = SR / 16;
+  static constexpr int PIECES = RB * KS;                  // 1 KiB pieces per stage
+  static constexpr int PPW = PIECES / 8;                  // ... per wave
+  static constexpr int STAGE = PIECES * 1024;
+  static constexpr int TGS = QW_NST * STAGE;              // [NST][8 waves][64 lanes] u32 bounds
+  static constexpr int TAU = TGS + QW_NST * 8 * 256;      // u64 tau_key[QT]
+  static constexpr int CNT = TAU + QW_QT * 8;             // int cnt[QT]
+  static constexpr int TOTAL = CNT + QW_QT * 4;
+  static_assert(SR > 0 && RB % 2 == 0 && PIECES % 8 == 0, "QW stage shape");
+  static_assert(TOTAL <= 160 * 1024, "LDS budget");
+};
+
+// the 2 fragments of a group: row blocks (2i, 2i+1) at one k-step = pieces p and p + KS,
+// issued with no wait (qw_frag_wait<N> waits and re-defines them)
+template <int KS, typename V>
+__device__ __forceinline__ void qw_issue_frags(uint32_t sbase, uint32_t voff, V (&av)[2]) {
+  uint32_t a;
+  asm volatile(
+      "v_add_u32 %2, %3, %4\n\t"
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %2 offset:%5"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(a)
+      : "s"(sbase), "v"(voff), "n"(KS * 1024)
+      : "memory");
+}
+template <int N, typename V>
+__device__ __forceinline__ void qw_frag_wait(V (&av)[2]) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(av[0]), "+v"(av[1]) : "n"(N) : "memory");
+}
+
+template <typename TM, int CAP, int KS>
+__global__ void __launch_bounds__(V3_NT, 1)
+score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
+                     const TM* __restrict__ qhat, int nqb, int P, int ntiles,
+                     uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
+  using L = QwLayout<KS>;
+  using Op = MfmaOp<TM>;
+  using V = typename Op::V;
+  constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = QW_NST, D = NST - 1;
+  constexpr int OPS = PPW + 1;                       // vmcnt-counted ops per wave per stage
+  constexpr int NG = (RB / 2) * KS;                  // fragment groups per stage
+  static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
+  __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
+  uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
+  int* cnt = reinterpret_cast<int*>(lds + L::CNT);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int qb = g % nqb, p = g / nqb;
+  const int t0 = (int)((int64_t)p * ntiles / P);
+  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
+  const int qbase = qb * QT;
+  uint64_t* wbuf = buf + (size_t)b * QT * CAP;
+  const int wq0 = wave * 32;                          // this wave's first query (block-local)
+  const int qlane = wq0 + (lane & 15);                // + 16 n: the query of accumulator block n
+
+  if (lane < 32) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
+  if (t0 >= t1) {
+    if (lane < 32) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
+    return;
+  }
+
+  // query fragments: lane l holds q^[qlane + 16 n][ks*32 + 8*(l >> 4) .. +8)
+  V qf[2][KS];
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const TM* src = qhat + (size_t)(qbase + qlane + 16 * n) * ld + (lane >> 4) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[n][ks] = *reinterpret_cast<const V*>(src + ks * 32);
+  }
+
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
+  const int ldb = ld * 2;
+  const int voff = drow * ldb + dchunk * 16;
+  const char* rows_b = reinterpret_cast<const char*>(rows);
+  const __amdgpu_buffer_rsrc_t tg_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(tau_g + qbase), (short)0, QT * 4, 0x00020000);
+
+  const int nsteps = t1 - t0;
+  // stage i (tile t0 + i) into ring slot i % NST: this wave's PPW row pieces (piece j = wave +
+  // 8 u: row block j / KS, k-step j % KS) and its 32 global bounds
+  auto issue_stage = [&](int i) __attribute__((always_inline)) {
+    const int slot = __builtin_amdgcn_readfirstlane(i % NST);
+    const int tile = __builtin_amdgcn_readfirstlane(t0 + i);
+    char* sa = lds + slot * L::STAGE;
+    const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        uniform_ptr(rows_b + (size_t)tile * SR * ldb), (short)0, SR * ldb, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int j = wave + 8 * u;
+      dma16(a_rsrc, sa + j * 1024, voff, (j / KS) * 16 * ldb + (j % KS) * (V3_BK * 2));
+    }
+    // the lane offset re-derived here (opaque to the compiler: hoisted, it was spilled and its
+    // reload waited for the ring)
+    int tv;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
+                 "v_and_b32 %0, 31, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(tv));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        tg_rsrc, (__attribute__((address_space(3))) void*)(lds + L::TGS + (slot * 8 + wave) * 256),
+        4, tv, wq0 * 4, 0, 0);
+  };
+  for (int i = 0; i < D; ++i)
+    if (i < nsteps) issue_stage(i);
+
+  const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
+  const uint32_t lds0 = lds_addr(lds);
+
+  bool need = false;
+  uint64_t tkr[2] = {0ull, 0ull};
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
+    if (s + D < nsteps) issue_stage(s + D);
+
+    const int slot = s % NST;
+    const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
+    floatx4 acc[RB][2];
+#pragma unroll
+    for (int m = 0; m < RB; ++m) acc[m][0] = acc[m][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // group j: row blocks (2 (j / KS), +1) at k-step j % KS; FD groups of reads in flight
+    constexpr int FD = 3;
+    auto gbase = [&](int j) { return st + (uint32_t)((2 * (j / KS) * KS + j % KS) * 1024); };
+    V av[FD][2];
+#pragma unroll
+    for (int j = 0; j < FD - 1; ++j) qw_issue_frags<KS, V>(gbase(j), offA, av[j]);
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      if (j + FD - 1 < NG) {
+        qw_issue_frags<KS, V>(gbase(j + FD - 1), offA, av[(j + FD - 1) % FD]);
+        qw_frag_wait<2 * (FD - 1)>(av[j % FD]);
+      } else if (j + 1 < NG) {
+        qw_frag_wait<2>(av[j % FD]);
+      } else {
+        qw_frag_wait<0>(av[j % FD]);
+      }
+      const int m0 = 2 * (j / KS), k0 = j % KS;
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[m0 + mm][n] = Op::run(av[j % FD][mm], qf[n][k0], acc[m0 + mm][n]);
+    }
+
+    // ---- epilogue of tile t0 + s: this wave's 32 queries x SR rows ----
+    int le;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
+    const int lq = le >> 4;
+    const int qle = wq0 + (le & 15);                 // the query of accumulator block 0
+    const int64_t row0 = (int64_t)(t0 + s) * SR;
+    if (row0 + SR > n_rows) {      // the corpus' last tile: rows past the end never pass (NaN)
+#pragma unroll
+      for (int m = 0; m < RB; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (row0 + m * 16 + lq * 4 + r >= n_rows) acc[m][0][r] = acc[m][1][r] = __builtin_nanf("");
+    }
+    float thr[2];
+    {
+      const uint32_t ta = lds_addr(lds + L::TGS + (slot * 8 + wave) * 256 + (le & 15) * 4);
+      uint32_t t0g, t1g;
+      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(t0g), "=&v"(t1g) : "v"(ta) : "memory");
+      thr[0] = fmaxf(tkr[0] ? key_score(tkr[0]) : -INFINITY, unord32(t0g));
+      thr[1] = fmaxf(tkr[1] ? key_score(tkr[1]) : -INFINITY, unord32(t1g));
+    }
+    bool hit[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int m = 0; m < RB; ++m)
+        mx = fmaxf(mx, fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])));
+      hit[n] = mx >= thr[n];
+    }
+    if (__any(hit[0] || hit[1])) {
+      const uint32_t row0u = (uint32_t)row0;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        if (!__any(hit[n])) continue;
+#pragma unroll
+        for (int m = 0; m < RB; ++m) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sc = acc[m][n][r];
+            const bool c = sc >= thr[n];
+            if (__builtin_amdgcn_ballot_w64(c)) {
+              if (c) {
+                const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
+                if (key > tkr[n]) {
+                  const int ql = qle + 16 * n;
+                  const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+                  wbuf[(size_t)ql * CAP + pos] = key;
+                  need |= pos + 1 > CAP - SR;
+                }
+              }
+            }
+          }
+        }
+      }
+      // a query whose buffer cannot take another tile's appends is compacted to its best k'
+      // (rare: drains this wave's stores and, in order, its ring pieces)
+      if (__any(need)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+        for (int ql = wq0; ql < wq0 + 32; ++ql) {
+          if ((int)v3_lds_u32(cnt + ql) > CAP - SR)
+            compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+                               tau_g + qbase + ql, kp, lane, nullptr);
+        }
+        need = false;
+        tkr[0] = v3_lds_u64(tau_key + qle);
+        tkr[1] = v3_lds_u64(tau_key + qle + 16);
+      }
+    }
+  }
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 32, kp, lane, partials, pcnt, P, p);
+}
+
+}  // namespace hcr

@@ -29,7 +29,8 @@ class SearchStats(ctypes.Structure):
                 ("uncertified_queries", c_int32), ("partitions", c_int32),
                 ("score_launches", c_int32), ("workgroups", c_int32),
                 ("score_kernel_ms", c_double), ("unit_kernel", c_int32),
-                ("fallback_queries", c_int32), ("fallback_rounds", c_int32)]
+                ("fallback_queries", c_int32), ("fallback_rounds", c_int32),
+                ("score_kernel", c_int32)]
 
 
 class BertConfig(ctypes.Structure):

@@ -140,6 +140,9 @@ typedef struct {
                                  product as coarse score, widened certificate bound) */
   int32_t fallback_queries;   /* queries answered by the exact fp64 scan (K6/K7) */
   int32_t fallback_rounds;    /* K6/K7 rounds run (threshold tightenings + 1 per group) */
+  int32_t score_kernel;       /* dense score kernel of the first pass: 1 register-staged
+                                 128 x 128 (fp32 rows), 3 v3 (256 x 16 / 256 x 64), 4 v4
+                                 (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
