@@ -483,17 +483,28 @@ def main():
     roof["traffic"] = load_traffic(a.traffic_file, N, D, nq, k, a.dtype, world)
     roof["traffic_unit"] = ("GB per score phase (rocprofv3 FETCH_SIZE+WRITE_SIZE passes of this "
                             "config, profiles/traffic_score.json)")
-    roof["kernel"] = ("score_topk_v4_kernel (fused MFMA score + top-k'): sample pre-pass + "
-                      "dense pass, HIP events around both on the library's stream")
+    kname = {1: "score_topk_kernel (register-staged 128 x 128)", 3: "score_topk_v3_kernel",
+             4: "score_topk_v4_kernel (256 x 256 tiles)",
+             5: "score_topk_qs_kernel (query-stationary, 128/256 queries per workgroup)",
+             6: "score_topk_qw_kernel (wide query-stationary: 256 queries per workgroup in VGPRs, "
+                "full-K row stages)"}.get(st.get("score_kernel", 0), "?")
+    roof["kernel"] = (kname + ", fused MFMA score + top-k': sample pre-pass (v4 MAXONLY) + dense "
+                      "pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
     roof["flops_per_launch"] = flops
     roof["alg_bytes_per_launch"] = bytes_alg
-    if nq >= 384:
+    ld = -(-D // 64) * 64
+    if st.get("score_kernel") == 6:
+        # QW's LDS fill: only rows, once per 256-query block (queries stay in VGPRs)
+        fill = nloc * ld * elt * (-(-nq // 256))
+        roof["lds_dma_fill_bytes"] = fill
+        roof["lds_dma_fill_TBps"] = round(fill / (avg_ms * 1e-3) / 1e12, 2)
+    elif st.get("score_kernel") == 4:
         # the 256 x 256 kernel's LDS fill: every stage brings 256 rows + 256 queries x 32 k
         # by LDS-DMA for 2*256*256*32 flop (128 flop per byte); the dense pass's rate of it
         # (the fill, not the MFMA pipe, bounds this tiling)
         n_tiles = -(-nloc // 256)
-        fill = n_tiles * (-(-nq // 256)) * 512 * D * elt
+        fill = n_tiles * (-(-nq // 256)) * 512 * ld * elt
         roof["lds_dma_fill_bytes"] = fill
         roof["lds_dma_fill_TBps"] = round(fill / (avg_ms * 1e-3) / 1e12, 2)
 
@@ -536,6 +547,7 @@ def main():
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
                       "widened_queries": widened, "fallback_queries": fallback,
                       "kprime": st["kprime"], "unit_kernel": st["unit_kernel"],
+                      "score_kernel": st.get("score_kernel"),
                       "partitions": st["partitions"], "workgroups": st["workgroups"],
                       "mfma_frac": round(flops / (avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
                       "hbm_frac_kernel": round(bytes_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -54,10 +54,12 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false; };
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, concat_split = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
+    // A/B hook: the reference-precision GEMMs as one concatenated depth-3K GEMM (gemm_v4)
+    t.concat_split = getenv("HCRAG_GEMM_CONCAT_SPLIT") != nullptr;
     if (const char* e = getenv("HCRAG_GEMM_FT")) t.gemm_ft = atoi(e);
     t.ln_scalar = getenv("HCRAG_LN_SCALAR") != nullptr;
     return t;
@@ -286,6 +288,24 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
   return HCR_OK;
 }
 
+// Reference-precision projection: C = oscale * (Xh.Wh 2^11 + Xh.Wl 2^11 + Xl 2^11.Wh) + bias (+
+// epilogue) from the split operands (row length 3 K), on gemm_split_kernel (4 distinct tiles
+// per stage instead of the concatenated GEMM's 6).  N is a multiple of 256 (weights padded to
+// 768-row multiples), T padded to 256.
+template <int EPI>
+static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N, int T,
+                             const float* bias, const float* resid, _Float16* out_h, float* out_f,
+                             int ldo, float oscale, hipStream_t st) {
+  if (enc_hooks().concat_split)
+    return launch_gemm<_Float16, EPI>(W, X, 3 * K, N, T, bias, resid, out_h, out_f, ldo, oscale, st);
+  if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
+  const int ntt = (int)(rup(T, G4_T) / G4_T), nft = (int)(rup(N, G4_T) / G4_T);
+  hipLaunchKernelGGL((gemm_split_kernel<EPI>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st, W, X,
+                     K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 template <typename TM, int DH, int KB>
 static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
                                  hipStream_t st) {
@@ -402,9 +422,9 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
   for (int l = 0; l < c.layers; ++l) {
     const EncLayer& L = e->layers[l];
     if constexpr (SPLIT) {
-      CHECK((launch_gemm<TM, EPI_BIAS_F32>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), 3 * H, 3 * H,
-                                           (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
-                                           e->qkv.as<float>(), 3 * H, L.sqkv, st)));
+      CHECK((launch_gemm_split<EPI_BIAS_F32>(L.wqkv.as<const _Float16>(), e->xh.as<const _Float16>(), H,
+                                             3 * H, (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
+                                             e->qkv.as<float>(), 3 * H, L.sqkv, st)));
       CHECK(launch_attention_f32(e, d_mask, n, S, st));
     } else {
       CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
@@ -412,22 +432,32 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
                                        3 * H, L.sqkv, st)));
       CHECK(launch_attention<TM>(e, d_mask, n, S, st));
     }
-    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H * w, H,
-                                           (int)T, L.bo.as<const float>(), e->x.as<const float>(),
-                                           nullptr, e->y.as<float>(), H, L.so, st)));
+    if constexpr (SPLIT)
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo.as<const _Float16>(), e->ctx.as<const _Float16>(), H, H,
+                                               (int)T, L.bo.as<const float>(), e->x.as<const float>(),
+                                               nullptr, e->y.as<float>(), H, L.so, st)));
+    else
+      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H,
+                                             (int)T, L.bo.as<const float>(), e->x.as<const float>(),
+                                             nullptr, e->y.as<float>(), H, L.so, st)));
     layer_norm(L.ln1g, L.ln1b);
     HIPC(hipGetLastError());
     if constexpr (SPLIT)
-      CHECK((launch_gemm<TM, EPI_BIAS_GELU_SPLIT>(L.wi.as<const TM>(), e->xh.as<const TM>(), 3 * H, F,
-                                                  (int)T, L.bi.as<const float>(), nullptr,
-                                                  e->inter.as<TM>(), nullptr, F, L.si, st)));
+      CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(L.wi.as<const _Float16>(), e->xh.as<const _Float16>(),
+                                                    H, F, (int)T, L.bi.as<const float>(), nullptr,
+                                                    (_Float16*)e->inter.as<TM>(), nullptr, F, L.si, st)));
     else
       CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
                                             L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
                                             nullptr, F, L.si, st)));
-    CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F * w, H,
-                                           (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
-                                           nullptr, e->y.as<float>(), H, L.so2, st)));
+    if constexpr (SPLIT)
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo2.as<const _Float16>(), e->inter.as<const _Float16>(), F,
+                                               H, (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
+                                               nullptr, e->y.as<float>(), H, L.so2, st)));
+    else
+      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F, H,
+                                             (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
+                                             nullptr, e->y.as<float>(), H, L.so2, st)));
     layer_norm(L.ln2g, L.ln2b);
     HIPC(hipGetLastError());
   }

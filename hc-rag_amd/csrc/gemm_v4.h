@@ -178,4 +178,169 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Reference-precision GEMM without the duplicated operand tiles.  The split operands are stored
+// X' = [Xh | Xh | Xl 2^11] and W' = [Wh 2^11 | Wl 2^11 | Wh] (row length 3K); gemm_v4_kernel
+// runs them as one GEMM of depth 3K, filling 6 tiles (Xh and Wh twice) for 3 products.  Here a
+// 32-deep stage fills the 4 distinct tiles -- Wh (segment 2), Wl 2^11 (segment 1), Xh (segment
+// 0), Xl 2^11 (segment 2) -- and runs the 3 products from them: Xl'.Wh, then Xh.(Wh 2^11) with
+// the Wh fragments scaled by 2^11 in registers (exact: |Wh| <= 16 after the upload's power-of-
+// two scale, so |Wh 2^11| <= 32768 < 65504), then Xh.Wl'.  Every product carries the same 2^11
+// as gemm_v4_kernel's, so `oscale` and the epilogues are unchanged.  LDS fill per MFMA flop is
+// 2/3 of the concatenated form (64 KiB per 3 x 256 x 256 x 32 products), 2 x 64 KiB ring.
+// 256-feature x 256-token tiles, 8 waves as gemm_v4_kernel (same fragment images and epilogue).
+__device__ __forceinline__ void g5_read4(uint32_t b, half8 (&bq)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:1024\n\t"
+      "ds_read_b128 %2, %4 offset:2048\n\t"
+      "ds_read_b128 %3, %4 offset:3072\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(bq[0]), "=&v"(bq[1]), "=&v"(bq[2]), "=&v"(bq[3])
+      : "v"(b)
+      : "memory");
+}
+__device__ __forceinline__ void g5_read8(uint32_t a, half8 (&av)[8]) {
+  asm volatile(
+      "ds_read_b128 %0, %8\n\t"
+      "ds_read_b128 %1, %8 offset:1024\n\t"
+      "ds_read_b128 %2, %8 offset:2048\n\t"
+      "ds_read_b128 %3, %8 offset:3072\n\t"
+      "ds_read_b128 %4, %8 offset:4096\n\t"
+      "ds_read_b128 %5, %8 offset:5120\n\t"
+      "ds_read_b128 %6, %8 offset:6144\n\t"
+      "ds_read_b128 %7, %8 offset:7168\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]),
+        "=&v"(av[6]), "=&v"(av[7])
+      : "v"(a)
+      : "memory");
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(V3_NT, 1)
+gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
+                  int T_real, int n_tiles_feat, const float* __restrict__ bias,
+                  const float* __restrict__ resid, _Float16* __restrict__ out_h,
+                  float* __restrict__ out_f, int ldo, float oscale) {
+  using Op = MfmaOp<_Float16>;
+  using V = half8;
+  constexpr int FT = G4_T, NST = 2;
+  constexpr int REG = FT * 64;                 // one 256-row x 32-k tile (16 KiB)
+  constexpr int WH = 0, WL = REG, XH = 2 * REG, XL = 3 * REG, STAGE = 4 * REG;
+  constexpr int MT = 8, NQ = 4, WN = 4;
+  __shared__ __attribute__((aligned(16))) char ring[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const int ft = g % n_tiles_feat, tt = g / n_tiles_feat;
+  const int f0 = ft * FT, t0 = tt * G4_T;
+
+  const int ldb = 3 * K * 2;                   // bytes per split row
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
+  const int voff = drow * ldb + dchunk * 16;
+  const int nsteps = K / V3_BK;
+  const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, FT * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(X) + (size_t)t0 * ldb), (short)0, G4_T * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(W), (short)0, 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(X), (short)0, 0, 0x00020000);
+
+  // piece i (0..7) of this wave for stage `is`: region i / 2 (Wh, Wl', Xh, Xl'), 16-row block
+  // wave + 8 (i % 2); kinds fixed per i (no runtime choice of descriptor)
+  auto issue_piece = [&](int is, int i) __attribute__((always_inline)) {
+    const bool live = is < nsteps;
+    const int kofs = __builtin_amdgcn_readfirstlane(is * (V3_BK * 2));
+    char* sa = ring + __builtin_amdgcn_readfirstlane(is & 1) * STAGE;
+    const int j = wave + 8 * (i & 1);
+    const int region = i >> 1;
+    const int seg = region == 0 ? 2 : region == 1 ? 1 : region == 2 ? 0 : 2;
+    if (region < 2)
+      dma16(live ? w_rsrc : w_null, sa + region * REG + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
+    else
+      dma16(live ? x_rsrc : x_null, sa + region * REG + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i) issue_piece(0, i);
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int fslot = v3_slot(fc, fr);
+  const int offA = (wm * (FT / 2) + fr) * 64 + fslot * 16;
+  const int offB = (wn * 64 + fr) * 64 + fslot * 16;
+  floatx4 acc[MT][NQ];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = 0; s < nsteps; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
+    const char* st = ring + (s & 1) * STAGE;
+    V av[MT], bq[NQ], bl[NQ];
+    g5_read8(lds_addr(st + WH + offA), av);
+    g5_read4(lds_addr(st + XL + offB), bl);
+    g5_read4(lds_addr(st + XH + offB), bq);
+    // Xl' . Wh
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+    issue_piece(s + 1, 0);
+    issue_piece(s + 1, 1);
+    issue_piece(s + 1, 2);
+    // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+    issue_piece(s + 1, 3);
+    issue_piece(s + 1, 4);
+    issue_piece(s + 1, 5);
+    // Xh . Wl'
+    g5_read8(lds_addr(st + WL + offA), av);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+    issue_piece(s + 1, 6);
+    issue_piece(s + 1, 7);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int f = f0 + wm * (FT / 2) + m * 16 + (lane >> 4) * 4;
+    if (f >= N_real) continue;
+    const float4 bb = *reinterpret_cast<const float4*>(bias + f);
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+      const int t = t0 + wn * 64 + n * 16 + (lane & 15);
+      if (t >= T_real) continue;
+      float v0 = fmaf(acc[m][n][0], oscale, bb.x), v1 = fmaf(acc[m][n][1], oscale, bb.y);
+      float v2 = fmaf(acc[m][n][2], oscale, bb.z), v3 = fmaf(acc[m][n][3], oscale, bb.w);
+      if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
+        v0 = gelu_exact(v0); v1 = gelu_exact(v1); v2 = gelu_exact(v2); v3 = gelu_exact(v3);
+        store_act4<_Float16, true>(out_h + (size_t)t * 3 * ldo, ldo, f, float4{v0, v1, v2, v3});
+      } else if constexpr (EPI == EPI_BIAS_RESID) {
+        const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
+        float4 o;
+        o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
+      } else {
+        static_assert(EPI == EPI_BIAS_F32, "split GEMM epilogues");
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = float4{v0, v1, v2, v3};
+      }
+    }
+  }
+}
+
 }  // namespace hcr

@@ -454,7 +454,7 @@ static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_c
 struct TestHooks {
   int64_t q64_elems = kQ64WideMaxElems;
   int qs_max = 256;
-  int qw_min = 257;
+  int qw_min = 0;                    // 0: the measured default (v3_cfg)
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
@@ -482,7 +482,12 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
-  if (nq >= hooks().qw_min && unit_ok && qw_ok && qw_supported(ld)) return {qw_rows(ld), kQwQueries, kQwStages, false, true};
+  // From 129 queries at D = 768 (r02 sweeps at 10M x 768: B = 160 3.64 vs 4.48 ms on QS,
+  // B = 256 3.73 vs 4.61); at D = 384 QS and QW tie at 129-256 (1M x 384, B = 256: 0.283 vs
+  // 0.282 ms), so QW from 257 there.
+  const int qw_from = hooks().qw_min > 0 ? hooks().qw_min : (ld / V3_BK >= 24 ? 129 : 257);
+  if (nq >= qw_from && unit_ok && qw_ok && qw_supported(ld))
+    return {qw_rows(ld), kQwQueries, kQwStages, false, true};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
   // LDS; 129-256 as two 128-query blocks per row partition).  Score ms, QS vs v3/v4
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42

@@ -14,7 +14,8 @@
 //    D = 384: 48 KiB), a 3-deep ring (two stages in flight), one barrier per stage;
 //  * the stage's LDS image is the v3 one (1 KiB pieces of 16 rows x 32 k, XOR-swizzled chunks):
 //    piece (rb, ks) at (rb x KS + ks) KiB; each wave DMAs 6 of the 48 pieces plus its 32 global
-//    bounds (a 4-byte-per-lane LDS-DMA: 7 vmcnt-counted ops per wave per stage);
+//    bounds (a 4-byte-per-lane LDS-DMA: 7 vmcnt-counted ops per wave per stage), issued right
+//    after the stage barrier;
 //  * per stage a wave runs RB x KS x 2 MFMAs (96 at D = 768: 1536 cycles) on 4 independent
 //    accumulator chains (row-block pair x query-block pair), fragment reads two groups ahead;
 //  * the epilogue is per stage (the accumulators of SR rows x 32 queries: 16 VGPRs), a max +
@@ -37,23 +38,24 @@ constexpr int QW_NST = 3;       // ring stages
 // rows per stage for KS 32-deep k-steps: 48 KiB stages (RB = SR / 16 row blocks, even)
 constexpr int qw_sr(int ks) { return ks == 24 ? 32 : ks == 12 ? 64 : 0; }
 
-template <int KS>
+template <int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST>
 struct QwLayout {
-  static constexpr int SR = qw_sr(KS), RB = SR / 16;
+  static constexpr int SR = SR_, RB = SR / 16, NST = NST_;
   static constexpr int PIECES = RB * KS;                  // 1 KiB pieces per stage
   static constexpr int PPW = PIECES / 8;                  // ... per wave
   static constexpr int STAGE = PIECES * 1024;
-  static constexpr int TGS = QW_NST * STAGE;              // [NST][8 waves][64 lanes] u32 bounds
-  static constexpr int TAU = TGS + QW_NST * 8 * 256;      // u64 tau_key[QT]
+  static constexpr int TGS = NST * STAGE;                 // [NST][8 waves][64 lanes] u32 bounds
+  static constexpr int TAU = TGS + NST * 8 * 256;         // u64 tau_key[QT]
   static constexpr int CNT = TAU + QW_QT * 8;             // int cnt[QT]
   static constexpr int TOTAL = CNT + QW_QT * 4;
-  static_assert(SR > 0 && RB % 2 == 0 && PIECES % 8 == 0, "QW stage shape");
+  static_assert(SR > 0 && (RB == 1 || RB % 2 == 0) && PIECES % 8 == 0, "QW stage shape");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
-// the 2 fragments of a group: row blocks (2i, 2i+1) at one k-step = pieces p and p + KS,
-// issued with no wait (qw_frag_wait<N> waits and re-defines them)
-template <int KS, typename V>
+// the 2 fragments of a group: pieces p and p + OFF2 KiB (row blocks 2i, 2i+1 at one k-step:
+// OFF2 = KS; or one row block at k-steps 2i, 2i+1: OFF2 = 1), issued with no wait
+// (qw_frag_wait<N> waits and re-defines them)
+template <int OFF2, typename V>
 __device__ __forceinline__ void qw_issue_frags(uint32_t sbase, uint32_t voff, V (&av)[2]) {
   uint32_t a;
   asm volatile(
@@ -61,7 +63,7 @@ __device__ __forceinline__ void qw_issue_frags(uint32_t sbase, uint32_t voff, V 
       "ds_read_b128 %0, %2\n\t"
       "ds_read_b128 %1, %2 offset:%5"
       : "=&v"(av[0]), "=&v"(av[1]), "=&v"(a)
-      : "s"(sbase), "v"(voff), "n"(KS * 1024)
+      : "s"(sbase), "v"(voff), "n"(OFF2 * 1024)
       : "memory");
 }
 template <int N, typename V>
@@ -69,18 +71,20 @@ __device__ __forceinline__ void qw_frag_wait(V (&av)[2]) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(av[0]), "+v"(av[1]) : "n"(N) : "memory");
 }
 
-template <typename TM, int CAP, int KS>
+template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = QwLayout<KS>;
+  using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
-  constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = QW_NST, D = NST - 1;
+  constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = L::NST, D = NST - 1;
   constexpr int OPS = PPW + 1;                       // vmcnt-counted ops per wave per stage
-  constexpr int NG = (RB / 2) * KS;                  // fragment groups per stage
+  // fragment groups per stage: (row-block pair, k-step), or (row block, k-step pair) if RB = 1
+  constexpr int NG = RB == 1 ? KS / 2 : (RB / 2) * KS;
+  constexpr int OFF2 = RB == 1 ? 1 : KS;
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -124,30 +128,43 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       uniform_ptr(tau_g + qbase), (short)0, QT * 4, 0x00020000);
 
   const int nsteps = t1 - t0;
-  // stage i (tile t0 + i) into ring slot i % NST: this wave's PPW row pieces (piece j = wave +
-  // 8 u: row block j / KS, k-step j % KS) and its 32 global bounds
-  auto issue_stage = [&](int i) __attribute__((always_inline)) {
-    const int slot = __builtin_amdgcn_readfirstlane(i % NST);
-    const int tile = __builtin_amdgcn_readfirstlane(t0 + i);
-    char* sa = lds + slot * L::STAGE;
-    const __amdgpu_buffer_rsrc_t a_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(rows_b + (size_t)tile * SR * ldb), (short)0, SR * ldb, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < PPW; ++u) {
-      const int j = wave + 8 * u;
-      dma16(a_rsrc, sa + j * 1024, voff, (j / KS) * 16 * ldb + (j % KS) * (V3_BK * 2));
-    }
-    // the lane offset re-derived here (opaque to the compiler: hoisted, it was spilled and its
-    // reload waited for the ring)
-    int tv;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
-                 "v_and_b32 %0, 31, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(tv));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        tg_rsrc, (__attribute__((address_space(3))) void*)(lds + L::TGS + (slot * 8 + wave) * 256),
-        4, tv, wq0 * 4, 0, 0);
+  // Stage i (tile t0 + i) goes to ring slot i % NST: this wave's PPW row pieces (piece j =
+  // wave + 8 u: row block j / KS, k-step j % KS) and its 32 global bounds -- OPS ops.  Stages
+  // past the partition's end are issued too, through zero-record descriptors (the loads return
+  // nothing and their LDS writes land in the slot of stage i - NST, already consumed), so every
+  // stage costs every wave exactly OPS vmcnt-counted ops and the loop has no tail cases.
+  struct StageDesc { __amdgpu_buffer_rsrc_t a, t; int slot; };
+  auto stage_desc = [&](int i) __attribute__((always_inline)) {
+    const bool live = i < nsteps;
+    StageDesc d;
+    d.slot = __builtin_amdgcn_readfirstlane(i % NST);
+    const int tile = __builtin_amdgcn_readfirstlane(t0 + (live ? i : 0));
+    d.a = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(rows_b + (size_t)tile * SR * ldb), (short)0,
+                                            live ? SR * ldb : 0, 0x00020000);
+    d.t = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(tau_g + qbase), (short)0, live ? QT * 4 : 0,
+                                            0x00020000);
+    return d;
   };
-  for (int i = 0; i < D; ++i)
-    if (i < nsteps) issue_stage(i);
+  auto issue_op = [&](const StageDesc& d, int u) __attribute__((always_inline)) {
+    if (u < PPW) {
+      const int j = wave + 8 * u;
+      dma16(d.a, lds + d.slot * L::STAGE + j * 1024, voff, (j / KS) * 16 * ldb + (j % KS) * (V3_BK * 2));
+    } else {
+      // the lane offset re-derived here (opaque to the compiler: hoisted, it was spilled and
+      // its reload waited for the ring)
+      int tv;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
+                   "v_and_b32 %0, 31, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(tv));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * 8 + wave) * 256),
+          4, tv, wq0 * 4, 0, 0);
+    }
+  };
+  for (int i = 0; i < D; ++i) {
+    const StageDesc d = stage_desc(i);
+#pragma unroll
+    for (int u = 0; u < OPS; ++u) issue_op(d, u);
+  }
 
   const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
   const uint32_t lds0 = lds_addr(lds);
@@ -155,38 +172,65 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   bool need = false;
   uint64_t tkr[2] = {0ull, 0ull};
   for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
-    if (s + D < nsteps) issue_stage(s + D);
+    // stage s + D into the slot everyone has finished with, all OPS ops at once: spread over the
+    // MFMA groups they cost 10 % fewer wave cycles but the 4 query blocks of a row partition
+    // drifted apart and FETCH_SIZE grew 2.6x (their shared L2 reuse broken: DESIGN.md §5)
+    {
+      const StageDesc nd = stage_desc(s + D);
+#pragma unroll
+      for (int u = 0; u < OPS; ++u) issue_op(nd, u);
+    }
 
     const int slot = s % NST;
     const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
+    // this stage's global bounds of the lane's two queries: read now, waited for with the
+    // last fragment group
+    uint32_t tg2[2];
+    {
+      int le0;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(le0) : "v"(lane));
+      const uint32_t ta = lds_addr(lds + L::TGS + (slot * 8 + wave) * 256 + (le0 & 15) * 4);
+      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64"
+                   : "=&v"(tg2[0]), "=&v"(tg2[1]) : "v"(ta) : "memory");
+    }
     floatx4 acc[RB][2];
 #pragma unroll
     for (int m = 0; m < RB; ++m) acc[m][0] = acc[m][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     // group j: row blocks (2 (j / KS), +1) at k-step j % KS; FD groups of reads in flight
     constexpr int FD = 3;
-    auto gbase = [&](int j) { return st + (uint32_t)((2 * (j / KS) * KS + j % KS) * 1024); };
+    auto gbase = [&](int j) {
+      return st + (uint32_t)((RB == 1 ? 2 * j : 2 * (j / KS) * KS + j % KS) * 1024);
+    };
     V av[FD][2];
 #pragma unroll
-    for (int j = 0; j < FD - 1; ++j) qw_issue_frags<KS, V>(gbase(j), offA, av[j]);
+    for (int j = 0; j < FD - 1; ++j) qw_issue_frags<OFF2, V>(gbase(j), offA, av[j]);
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
       if (j + FD - 1 < NG) {
-        qw_issue_frags<KS, V>(gbase(j + FD - 1), offA, av[(j + FD - 1) % FD]);
+        qw_issue_frags<OFF2, V>(gbase(j + FD - 1), offA, av[(j + FD - 1) % FD]);
         qw_frag_wait<2 * (FD - 1)>(av[j % FD]);
       } else if (j + 1 < NG) {
         qw_frag_wait<2>(av[j % FD]);
       } else {
         qw_frag_wait<0>(av[j % FD]);
+        asm volatile("" : "+v"(tg2[0]), "+v"(tg2[1]));   // (read before the fragments: landed)
       }
-      const int m0 = 2 * (j / KS), k0 = j % KS;
+      if constexpr (RB == 1) {
 #pragma unroll
-      for (int mm = 0; mm < 2; ++mm)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[m0 + mm][n] = Op::run(av[j % FD][mm], qf[n][k0], acc[m0 + mm][n]);
+          for (int n = 0; n < 2; ++n)
+            acc[0][n] = Op::run(av[j % FD][kk], qf[n][2 * j + kk], acc[0][n]);
+      } else {
+        const int m0 = 2 * (j / KS), k0 = j % KS;
+#pragma unroll
+        for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+            acc[m0 + mm][n] = Op::run(av[j % FD][mm], qf[n][k0], acc[m0 + mm][n]);
+      }
     }
 
     // ---- epilogue of tile t0 + s: this wave's 32 queries x SR rows ----
@@ -203,14 +247,8 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
           if (row0 + m * 16 + lq * 4 + r >= n_rows) acc[m][0][r] = acc[m][1][r] = __builtin_nanf("");
     }
     float thr[2];
-    {
-      const uint32_t ta = lds_addr(lds + L::TGS + (slot * 8 + wave) * 256 + (le & 15) * 4);
-      uint32_t t0g, t1g;
-      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(t0g), "=&v"(t1g) : "v"(ta) : "memory");
-      thr[0] = fmaxf(tkr[0] ? key_score(tkr[0]) : -INFINITY, unord32(t0g));
-      thr[1] = fmaxf(tkr[1] ? key_score(tkr[1]) : -INFINITY, unord32(t1g));
-    }
+    thr[0] = fmaxf(tkr[0] ? key_score(tkr[0]) : -INFINITY, unord32(tg2[0]));
+    thr[1] = fmaxf(tkr[1] ? key_score(tkr[1]) : -INFINITY, unord32(tg2[1]));
     bool hit[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {

@@ -12,9 +12,9 @@ using namespace hcr;
 
 namespace {
 
-template <typename TM, int CAP, int KS>
+template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                      static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
                      a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
@@ -39,7 +39,7 @@ bool by_cap(const QsArgs& a, hipStream_t st) {
 
 bool qw_supported(int ld) { return ld % V3_BK == 0 && qw_sr(ld / V3_BK) > 0; }
 int qw_rows(int ld) { return qw_sr(ld / V3_BK); }
-int qw_cap(int kp, int ld) { return kp + qw_rows(ld) <= 256 ? 256 : 0; }   // 0: not supported
+int qw_cap(int kp, int ld) { return kp + qw_sr(ld / V3_BK) <= 256 ? 256 : 0; }   // 0: not supported
 
 int launch_qw(int dtype, const QsArgs& a, hipStream_t st) {
   const bool ok = dtype == HCR_F16 ? by_cap<_Float16>(a, st) : by_cap<__bf16>(a, st);
