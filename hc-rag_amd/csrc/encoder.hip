@@ -54,12 +54,10 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, concat_split = false; };
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
-    // A/B hook: the reference-precision GEMMs as one concatenated depth-3K GEMM (gemm_v4)
-    t.concat_split = getenv("HCRAG_GEMM_CONCAT_SPLIT") != nullptr;
     if (const char* e = getenv("HCRAG_GEMM_FT")) t.gemm_ft = atoi(e);
     t.ln_scalar = getenv("HCRAG_LN_SCALAR") != nullptr;
     return t;
@@ -296,8 +294,6 @@ template <int EPI>
 static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N, int T,
                              const float* bias, const float* resid, _Float16* out_h, float* out_f,
                              int ldo, float oscale, hipStream_t st) {
-  if (enc_hooks().concat_split)
-    return launch_gemm<_Float16, EPI>(W, X, 3 * K, N, T, bias, resid, out_h, out_f, ldo, oscale, st);
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
   const int ntt = (int)(rup(T, G4_T) / G4_T), nft = (int)(rup(N, G4_T) / G4_T);
   hipLaunchKernelGGL((gemm_split_kernel<EPI>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st, W, X,

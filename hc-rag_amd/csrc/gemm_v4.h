@@ -1,10 +1,9 @@
 // gemm_v4.h — encoder projection GEMM on the LDS-DMA ring of the v4 score kernel
 // (score_v4.h): C[token][feature] = X[token][:] · W[feature][:] + bias (+ GELU | + residual).
 //
-// Reference-precision mode: X = [Xh | Xh | Xl*2^11] and W = [Wh*2^11 | Wl*2^11 | Wh] (K = 3 x
-// the model width, encoder_kernels.h store_act4 / to_split_weights) make the same kernel
-// compute 2^11 (Xh Wh + Xh Wl + Xl Wh); `oscale` undoes that factor and the weights' power-of-
-// two scale (1 in the fast modes: fma(acc, 1, bias) = acc + bias exactly).
+// Fast modes (f16 / bf16 operands).  The reference-precision mode's split operands run on
+// gemm_split_kernel below; `oscale` undoes the split's 2^11 and the weights' power-of-two scale
+// (1 in the fast modes: fma(acc, 1, bias) = acc + bias exactly).
 //
 // One workgroup = one 256-feature x 256-token output tile over the whole K; 8 waves (2 x 4),
 // each 128 features x 64 tokens as 8 x 4 16x16x32 MFMA blocks; K = 32 per stage, NST-stage
@@ -179,9 +178,9 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Reference-precision GEMM without the duplicated operand tiles.  The split operands are stored
-// X' = [Xh | Xh | Xl 2^11] and W' = [Wh 2^11 | Wl 2^11 | Wh] (row length 3K); gemm_v4_kernel
-// runs them as one GEMM of depth 3K, filling 6 tiles (Xh and Wh twice) for 3 products.  Here a
+// Reference-precision GEMM without duplicated operand tiles.  The split operands are stored
+// X' = [Xh | - | Xl 2^11] and W' = [Wh 2^11 | Wl 2^11 | Wh] (row length 3K); run as one GEMM of
+// depth 3K over [Xh | Xh | Xl'] they needed 6 tiles (Xh and Wh twice) for 3 products.  Here a
 // 32-deep stage fills the 4 distinct tiles -- Wh (segment 2), Wl 2^11 (segment 1), Xh (segment
 // 0), Xl 2^11 (segment 2) -- and runs the 3 products from them: Xl'.Wh, then Xh.(Wh 2^11) with
 // the Wh fragments scaled by 2^11 in registers (exact: |Wh| <= 16 after the upload's power-of-
