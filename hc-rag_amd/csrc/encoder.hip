@@ -288,16 +288,30 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 
 // Reference-precision projection: C = oscale * (Xh.Wh 2^11 + Xh.Wl 2^11 + Xl 2^11.Wh) + bias (+
 // epilogue) from the split operands (row length 3 K), on gemm_split_kernel (4 distinct tiles
-// per stage instead of the concatenated GEMM's 6).  N is a multiple of 256 (weights padded to
-// 768-row multiples), T padded to 256.
+// per stage instead of the concatenated GEMM's 6).  Weights are padded to 768-row multiples (a
+// whole number of 256- or 192-feature tiles), T padded to 256.
 template <int EPI>
 static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N, int T,
                              const float* bias, const float* resid, _Float16* out_h, float* out_f,
                              int ldo, float oscale, hipStream_t st) {
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
-  const int ntt = (int)(rup(T, G4_T) / G4_T), nft = (int)(rup(N, G4_T) / G4_T);
-  hipLaunchKernelGGL((gemm_split_kernel<EPI>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st, W, X,
-                     K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  const int ntt = (int)(rup(T, G4_T) / G4_T);
+  // 192-feature tiles where they fill whole rounds of 256 resident workgroups and 256-wide
+  // ones do not (N = 768 at T = 32768: 512 tiles = 2 rounds vs 384 = 1.5).  A round of 192
+  // tiles costs ~0.86 of a 256 one (r02, bge-base T = 32768: QKV 6 rounds 354 us vs 5 rounds
+  // 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
+  auto rounds = [&](int ft) { return (double)((rup(N, ft) / ft * (int64_t)ntt + 255) / 256); };
+  const int force_ft = enc_hooks().gemm_ft;
+  const bool ft192 = force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256);
+  if (ft192) {
+    const int nft = (int)(rup(N, 192) / 192);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, 192>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st,
+                       W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  } else {
+    const int nft = (int)(rup(N, G4_T) / G4_T);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st,
+                       W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  }
   HIPC(hipGetLastError());
   return HCR_OK;
 }

@@ -216,7 +216,23 @@ __device__ __forceinline__ void g5_read8(uint32_t a, half8 (&av)[8]) {
       : "memory");
 }
 
-template <int EPI>
+// FT = 256, or 192 for N = 768 (4 x 128 tiles at T = 32768 fill 2 rounds of 256 CUs exactly;
+// 256-feature tiles leave the second of 2 rounds half empty).
+__device__ __forceinline__ void g5_read6(uint32_t a, half8 (&av)[6]) {
+  asm volatile(
+      "ds_read_b128 %0, %6\n\t"
+      "ds_read_b128 %1, %6 offset:1024\n\t"
+      "ds_read_b128 %2, %6 offset:2048\n\t"
+      "ds_read_b128 %3, %6 offset:3072\n\t"
+      "ds_read_b128 %4, %6 offset:4096\n\t"
+      "ds_read_b128 %5, %6 offset:5120\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5])
+      : "v"(a)
+      : "memory");
+}
+
+template <int EPI, int FT = G4_T>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
@@ -224,10 +240,13 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
                   float* __restrict__ out_f, int ldo, float oscale) {
   using Op = MfmaOp<_Float16>;
   using V = half8;
-  constexpr int FT = G4_T, NST = 2;
-  constexpr int REG = FT * 64;                 // one 256-row x 32-k tile (16 KiB)
-  constexpr int WH = 0, WL = REG, XH = 2 * REG, XL = 3 * REG, STAGE = 4 * REG;
-  constexpr int MT = 8, NQ = 4, WN = 4;
+  static_assert(FT == 256 || FT == 192, "feature tile");
+  constexpr int NST = 2;
+  constexpr int REGW = FT * 64, REGX = G4_T * 64;   // one FT- / 256-row x 32-k tile
+  constexpr int WH = 0, WL = REGW, XH = 2 * REGW, XL = 2 * REGW + REGX, STAGE = 2 * REGW + 2 * REGX;
+  constexpr int MT = FT / 32, NQ = 4, WN = 4;
+  constexpr int NPW = FT / 16;                      // pieces per W region (16 or 12)
+  constexpr int PPW = (2 * NPW + 32) / 8;           // pieces per wave per stage (8 or 7)
   __shared__ __attribute__((aligned(16))) char ring[NST * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -251,22 +270,34 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   const __amdgpu_buffer_rsrc_t w_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(W), (short)0, 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t x_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(X), (short)0, 0, 0x00020000);
 
-  // piece i (0..7) of this wave for stage `is`: region i / 2 (Wh, Wl', Xh, Xl'), 16-row block
-  // wave + 8 (i % 2); kinds fixed per i (no runtime choice of descriptor)
+  // piece i (0 .. PPW-1) of this wave for stage `is`.  FT = 256: region i / 2 (Wh, Wl', Xh,
+  // Xl'), 16-row block wave + 8 (i % 2).  FT = 192: i = 0 Wh block wave; i = 1 Wh block 8 +
+  // wave (waves 0-3) or Wl block wave - 4 (waves 4-7: same W descriptor, a wave-uniform
+  // choice of offsets); i = 2 Wl block 4 + wave; i = 3, 4 Xh; i = 5, 6 Xl.  The segment of the
+  // split rows: Wh = 2, Wl' = 1, Xh = 0, Xl' = 2.
   auto issue_piece = [&](int is, int i) __attribute__((always_inline)) {
     const bool live = is < nsteps;
     const int kofs = __builtin_amdgcn_readfirstlane(is * (V3_BK * 2));
     char* sa = ring + __builtin_amdgcn_readfirstlane(is & 1) * STAGE;
-    const int j = wave + 8 * (i & 1);
-    const int region = i >> 1;
+    int region, j;
+    if constexpr (FT == 256) {
+      region = i >> 1;
+      j = wave + 8 * (i & 1);
+    } else {
+      if (i == 0) { region = 0; j = wave; }
+      else if (i == 1) { region = wave < 4 ? 0 : 1; j = wave < 4 ? 8 + wave : wave - 4; }
+      else if (i == 2) { region = 1; j = 4 + wave; }
+      else { region = 2 + (i - 3) / 2; j = wave + 8 * ((i - 3) & 1); }
+    }
     const int seg = region == 0 ? 2 : region == 1 ? 1 : region == 2 ? 0 : 2;
+    const int rbase = region == 0 ? WH : region == 1 ? WL : region == 2 ? XH : XL;
     if (region < 2)
-      dma16(live ? w_rsrc : w_null, sa + region * REG + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
+      dma16(live ? w_rsrc : w_null, sa + rbase + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
     else
-      dma16(live ? x_rsrc : x_null, sa + region * REG + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
+      dma16(live ? x_rsrc : x_null, sa + rbase + j * 1024, voff, j * 16 * ldb + seg * 2 * K + kofs);
   };
 #pragma unroll
-  for (int i = 0; i < 8; ++i) issue_piece(0, i);
+  for (int i = 0; i < PPW; ++i) issue_piece(0, i);
 
   const int fr = lane & 15, fc = lane >> 4;
   const int fslot = v3_slot(fc, fr);
@@ -283,7 +314,8 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
     const char* st = ring + (s & 1) * STAGE;
     V av[MT], bq[NQ], bl[NQ];
-    g5_read8(lds_addr(st + WH + offA), av);
+    if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
+    else g5_read6(lds_addr(st + WH + offA), av);
     g5_read4(lds_addr(st + XL + offB), bl);
     g5_read4(lds_addr(st + XH + offB), bq);
     // Xl' . Wh
@@ -305,13 +337,14 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     issue_piece(s + 1, 4);
     issue_piece(s + 1, 5);
     // Xh . Wl'
-    g5_read8(lds_addr(st + WL + offA), av);
+    if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
+    else g5_read6(lds_addr(st + WL + offA), av);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
     issue_piece(s + 1, 6);
-    issue_piece(s + 1, 7);
+    if constexpr (PPW == 8) issue_piece(s + 1, 7);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
