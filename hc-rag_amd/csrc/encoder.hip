@@ -54,12 +54,14 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false; };
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
     if (const char* e = getenv("HCRAG_GEMM_FT")) t.gemm_ft = atoi(e);
     t.ln_scalar = getenv("HCRAG_LN_SCALAR") != nullptr;
+    // reference-precision FFN1 GELU with the library erff instead of erf_as
+    t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     return t;
   }();
   return h;
@@ -303,14 +305,21 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
   auto rounds = [&](int ft) { return (double)((rup(N, ft) / ft * (int64_t)ntt + 255) / 256); };
   const int force_ft = enc_hooks().gemm_ft;
   const bool ft192 = force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256);
-  if (ft192) {
-    const int nft = (int)(rup(N, 192) / 192);
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, 192>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st,
-                       W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  const int nft = (int)(rup(N, ft192 ? 192 : G4_T) / (ft192 ? 192 : G4_T));
+  const dim3 grid((unsigned)(nft * ntt));
+  if (EPI == EPI_BIAS_GELU_SPLIT && enc_hooks().gelu_liberf) {
+    if (ft192)
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, 192, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
+                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
+    else
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
+                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
+  } else if (ft192) {
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, 192>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, nft,
+                       bias, resid, out_h, out_f, ldo, oscale);
   } else {
-    const int nft = (int)(rup(N, G4_T) / G4_T);
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), dim3((unsigned)(nft * ntt)), dim3(V3_NT), 0, st,
-                       W, X, K, N, T, nft, bias, resid, out_h, out_f, ldo, oscale);
+    hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, nft,
+                       bias, resid, out_h, out_f, ldo, oscale);
   }
   HIPC(hipGetLastError());
   return HCR_OK;

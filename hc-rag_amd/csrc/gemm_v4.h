@@ -232,7 +232,9 @@ __device__ __forceinline__ void g5_read6(uint32_t a, half8 (&av)[6]) {
       : "memory");
 }
 
-template <int EPI, int FT = G4_T>
+// LIBERF: the FFN1 epilogue's GELU with the library erff (~50 instructions) instead of erf_as
+// (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
+template <int EPI, int FT = G4_T, bool LIBERF = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
@@ -360,7 +362,11 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
       float v0 = fmaf(acc[m][n][0], oscale, bb.x), v1 = fmaf(acc[m][n][1], oscale, bb.y);
       float v2 = fmaf(acc[m][n][2], oscale, bb.z), v3 = fmaf(acc[m][n][3], oscale, bb.w);
       if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
-        v0 = gelu_exact(v0); v1 = gelu_exact(v1); v2 = gelu_exact(v2); v3 = gelu_exact(v3);
+        if constexpr (LIBERF) {
+          v0 = gelu_exact(v0); v1 = gelu_exact(v1); v2 = gelu_exact(v2); v3 = gelu_exact(v3);
+        } else {
+          v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+        }
         store_act4<_Float16, true>(out_h + (size_t)t * 3 * ldo, ldo, f, float4{v0, v1, v2, v3});
       } else if constexpr (EPI == EPI_BIAS_RESID) {
         const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
