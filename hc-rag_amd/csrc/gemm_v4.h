@@ -350,6 +350,65 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
+  if constexpr (EPI == EPI_BIAS_GELU_SPLIT && FT == 256) {
+    // FFN1: the split activations (h, l) go out through LDS.  Stored straight from the
+    // accumulators a lane writes 4 features of one token: 32-B pieces of 16 different rows per
+    // instruction, half-line writes on ~400 MB per launch.  Here each wave stages 64 features x
+    // 64 tokens of h and of l (8 KiB each, 16-B granules XOR-swizzled by token) in its 16 KiB of
+    // the now idle ring, then writes 128-B row pieces: 8 lanes per token row.
+    __syncthreads();                               // every wave done with the ring
+    char* hs = ring + wave * 16384;
+    char* ls = hs + 8192;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int m = hh * 4 + mi;
+        const int fl = mi * 16 + (lane >> 4) * 4;               // feature within the 64
+        const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * 128 + hh * 64 + fl);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          const int tl = n * 16 + (lane & 15);                  // token within the 64
+          float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                        fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+          union { _Float16 e[4]; uint2 u; } ph, pl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = LIBERF ? gelu_exact(v[r]) : gelu_erf(v[r]);
+            ph.e[r] = (_Float16)v[r];
+            pl.e[r] = (_Float16)((v[r] - (float)ph.e[r]) * kSplitLo);
+          }
+          const int off = tl * 128 + (((fl >> 3) ^ (tl & 7)) << 4) + (fl & 7) * 2;
+          *reinterpret_cast<uint2*>(hs + off) = ph.u;
+          *reinterpret_cast<uint2*>(ls + off) = pl.u;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // 64 rows x 8 granules: 8 rows per instruction, lane -> (row lane / 8, granule lane % 8)
+      const int gr = lane & 7;
+      const int fcol = f0 + wm * 128 + hh * 64 + gr * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int tl = i * 8 + (lane >> 3);
+        const int t = t0 + wn * 64 + tl;
+        const int off = tl * 128 + ((gr ^ (tl & 7)) << 4);
+        const uint4 h4 = *reinterpret_cast<const uint4*>(hs + off);
+        const uint4 l4 = *reinterpret_cast<const uint4*>(ls + off);
+        if (t < T_real && fcol < N_real) {
+          _Float16* row = out_h + (size_t)t * 3 * ldo;
+          *reinterpret_cast<uint4*>(row + fcol) = h4;
+          *reinterpret_cast<uint4*>(row + 2 * ldo + fcol) = l4;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return;
+  }
+
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int f = f0 + wm * (FT / 2) + m * 16 + (lane >> 4) * 4;
