@@ -304,16 +304,18 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
   // 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
   auto rounds = [&](int ft) { return (double)((rup(N, ft) / ft * (int64_t)ntt + 255) / 256); };
   const int force_ft = enc_hooks().gemm_ft;
-  const bool ft192 = force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256);
+  // (FFN1's epilogue stages 64-feature halves: 256-feature tiles only)
+  constexpr bool can192 = EPI != EPI_BIAS_GELU_SPLIT;
+  const bool ft192 = can192 && (force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256));
   const int nft = (int)(rup(N, ft192 ? 192 : G4_T) / (ft192 ? 192 : G4_T));
   const dim3 grid((unsigned)(nft * ntt));
-  if (EPI == EPI_BIAS_GELU_SPLIT && enc_hooks().gelu_liberf) {
-    if (ft192)
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, 192, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
-                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
-    else
+  if constexpr (!can192) {
+    if (enc_hooks().gelu_liberf)
       hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
                          T, nft, bias, resid, out_h, out_f, ldo, oscale);
+    else
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
+                         nft, bias, resid, out_h, out_f, ldo, oscale);
   } else if (ft192) {
     hipLaunchKernelGGL((gemm_split_kernel<EPI, 192>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, nft,
                        bias, resid, out_h, out_f, ldo, oscale);

@@ -350,7 +350,8 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if constexpr (EPI == EPI_BIAS_GELU_SPLIT && FT == 256) {
+  if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
+    static_assert(FT == 256, "the FFN1 epilogue stages 64-feature halves of a 128-feature wave");
     // FFN1: the split activations (h, l) go out through LDS.  Stored straight from the
     // accumulators a lane writes 4 features of one token: 32-B pieces of 16 different rows per
     // instruction, half-line writes on ~400 MB per launch.  Here each wave stages 64 features x
@@ -409,34 +410,58 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     return;
   }
 
+  // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well: per chunk of 2 row
+  // blocks a wave stages 32 features x 64 tokens (8 KiB, 16-B granules XOR-swizzled by token)
+  // and writes -- reading the residual alongside -- 128-B row pieces (from the accumulators
+  // each store covered 64 B of 16 rows)
+  else {
+  static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
+  __syncthreads();                                 // every wave done with the ring
+  char* vs = ring + wave * 8192;
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int f = f0 + wm * (FT / 2) + m * 16 + (lane >> 4) * 4;
-    if (f >= N_real) continue;
-    const float4 bb = *reinterpret_cast<const float4*>(bias + f);
+  for (int c = 0; c < MT / 2; ++c) {
 #pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-      const int t = t0 + wn * 64 + n * 16 + (lane & 15);
-      if (t >= T_real) continue;
-      float v0 = fmaf(acc[m][n][0], oscale, bb.x), v1 = fmaf(acc[m][n][1], oscale, bb.y);
-      float v2 = fmaf(acc[m][n][2], oscale, bb.z), v3 = fmaf(acc[m][n][3], oscale, bb.w);
-      if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
-        if constexpr (LIBERF) {
-          v0 = gelu_exact(v0); v1 = gelu_exact(v1); v2 = gelu_exact(v2); v3 = gelu_exact(v3);
-        } else {
-          v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-        }
-        store_act4<_Float16, true>(out_h + (size_t)t * 3 * ldo, ldo, f, float4{v0, v1, v2, v3});
-      } else if constexpr (EPI == EPI_BIAS_RESID) {
-        const float4 rr = *reinterpret_cast<const float4*>(resid + (size_t)t * ldo + f);
-        float4 o;
-        o.x = v0 + rr.x; o.y = v1 + rr.y; o.z = v2 + rr.z; o.w = v3 + rr.w;
-        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = o;
-      } else {
-        static_assert(EPI == EPI_BIAS_F32, "split GEMM epilogues");
-        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + f) = float4{v0, v1, v2, v3};
+    for (int mi = 0; mi < 2; ++mi) {
+      const int m = 2 * c + mi;
+      const int fl = mi * 16 + (lane >> 4) * 4;                 // feature within the 32
+      const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * (FT / 2) + c * 32 + fl);
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        const int tl = n * 16 + (lane & 15);
+        const float4 v = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                          fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+        *reinterpret_cast<float4*>(vs + tl * 128 + (((fl >> 2) ^ (tl & 7)) << 4)) = v;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int gr = lane & 7;
+    const int fcol = f0 + wm * (FT / 2) + c * 32 + gr * 4;
+    // the 8 rows' residual pieces loaded together (one wait), then add + store
+    float4 rr[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = t0 + wn * 64 + i * 8 + (lane >> 3);
+      rr[i] = float4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS_RESID)   // clamped into the matrix: unconditional loads
+        rr[i] = *reinterpret_cast<const float4*>(resid + (size_t)min(t, T_real - 1) * ldo +
+                                                 min(fcol, N_real - 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int tl = i * 8 + (lane >> 3);
+      const int t = t0 + wn * 64 + tl;
+      float4 v = *reinterpret_cast<const float4*>(vs + tl * 128 + ((gr ^ (tl & 7)) << 4));
+      if (t < T_real && fcol < N_real) {
+        v.x += rr[i].x; v.y += rr[i].y; v.z += rr[i].z; v.w += rr[i].w;
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + fcol) = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
   }
 }
 
