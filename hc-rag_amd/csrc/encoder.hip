@@ -263,6 +263,7 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
                        const float* resid, TM* out_h, float* out_f, int ldo, float oscale,
                        hipStream_t st) {
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
+  if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
   // feature tile: 192 when it fills the last round of 256-CU workgroups better than 256
   // (N = 768 at T = 32768: 512 tiles = 2 full rounds vs 384 = 1.5); weights are padded to
   // a multiple of 768 rows so either tile reads whole rows.
@@ -297,6 +298,7 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
                              const float* bias, const float* resid, _Float16* out_h, float* out_f,
                              int ldo, float oscale, hipStream_t st) {
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
+  if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
   const int ntt = (int)(rup(T, G4_T) / G4_T);
   // 192-feature tiles where they fill whole rounds of 256 resident workgroups and 256-wide
   // ones do not (N = 768 at T = 32768: 512 tiles = 2 rounds vs 384 = 1.5).  A round of 192

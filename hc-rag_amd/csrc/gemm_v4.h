@@ -20,6 +20,101 @@ namespace hcr {
 
 constexpr int G4_T = 256;     // features and tokens per tile
 
+// Output epilogues staged through LDS (the tile's ring, idle after the main loop): from the
+// accumulators a lane holds 4 features of one token, so a direct store covers 16 rows x 16 B
+// (fp32) or 16 rows x 8 B (16-bit) per instruction; staged, each wave writes its tile's rows as
+// 128-B (fp32) or 64-B (16-bit) pieces.  Per chunk of 2 row blocks a wave stages 32 features x
+// 64 tokens in its own `vs` (8 KiB; 16-B granules XOR-swizzled by token), then reads back 8
+// (fp32) or 16 (16-bit) rows per instruction.  fbase / tbase: the wave's first feature / token.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int EPI, int MT>
+__device__ __forceinline__ void staged_epilogue_f32(char* vs, int lane, const floatx4 (&acc)[MT][4],
+                                                    int fbase, int tbase, int N_real, int T_real,
+                                                    const float* __restrict__ bias,
+                                                    const float* __restrict__ resid,
+                                                    float* __restrict__ out_f, int ldo, float oscale) {
+#pragma unroll
+  for (int c = 0; c < MT / 2; ++c) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int m = 2 * c + mi;
+      const int fl = mi * 16 + (lane >> 4) * 4;
+      const float4 bb = *reinterpret_cast<const float4*>(bias + min(fbase + c * 32 + fl, N_real - 4));
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int tl = n * 16 + (lane & 15);
+        const float4 v = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                          fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+        *reinterpret_cast<float4*>(vs + tl * 128 + (((fl >> 2) ^ (tl & 7)) << 4)) = v;
+      }
+    }
+    wave_lds_sync();
+    const int gr = lane & 7;
+    const int fcol = fbase + c * 32 + gr * 4;
+    // the 8 rows' residual pieces loaded together (one wait), clamped into the matrix
+    float4 rr[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = tbase + i * 8 + (lane >> 3);
+      rr[i] = float4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS_RESID)
+        rr[i] = *reinterpret_cast<const float4*>(resid + (size_t)min(t, T_real - 1) * ldo +
+                                                 min(fcol, N_real - 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int tl = i * 8 + (lane >> 3);
+      const int t = tbase + tl;
+      float4 v = *reinterpret_cast<const float4*>(vs + tl * 128 + ((gr ^ (tl & 7)) << 4));
+      if (t < T_real && fcol < N_real) {
+        v.x += rr[i].x; v.y += rr[i].y; v.z += rr[i].z; v.w += rr[i].w;
+        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + fcol) = v;
+      }
+    }
+    wave_lds_sync();
+  }
+}
+template <typename TM, bool GELU, int MT>
+__device__ __forceinline__ void staged_epilogue_h(char* vs, int lane, const floatx4 (&acc)[MT][4],
+                                                  int fbase, int tbase, int N_real, int T_real,
+                                                  const float* __restrict__ bias,
+                                                  TM* __restrict__ out_h, int ldo, float oscale) {
+#pragma unroll
+  for (int c = 0; c < MT / 2; ++c) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int m = 2 * c + mi;
+      const int fl = mi * 16 + (lane >> 4) * 4;              // 4 features = half a 16-B granule
+      const float4 bb = *reinterpret_cast<const float4*>(bias + min(fbase + c * 32 + fl, N_real - 4));
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int tl = n * 16 + (lane & 15);
+        float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                      fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+        union { TM e[4]; uint2 u; } ph;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ph.e[r] = (TM)(GELU ? gelu_erf(v[r]) : v[r]);
+        *reinterpret_cast<uint2*>(vs + tl * 64 + (((fl >> 3) ^ (tl & 3)) << 4) + (fl & 7) * 2) = ph.u;
+      }
+    }
+    wave_lds_sync();
+    const int gr = lane & 3;
+    const int fcol = fbase + c * 32 + gr * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int tl = i * 16 + (lane >> 2);
+      const int t = tbase + tl;
+      const uint4 v = *reinterpret_cast<const uint4*>(vs + tl * 64 + ((gr ^ (tl & 3)) << 4));
+      if (t < T_real && fcol < N_real) *reinterpret_cast<uint4*>(out_h + (size_t)t * ldo + fcol) = v;
+    }
+    wave_lds_sync();
+  }
+}
+
 // FT = features per tile: 256 (8 row blocks per wave) or 192 (6), the latter for N = 768 /
 // 2304 where 256-wide tiles leave the last round of workgroups half empty (1.5 and 4.5 rounds
 // of 256 CUs at T = 32768 tokens).
@@ -144,6 +239,18 @@ gemm_v4_kernel(const TM* __restrict__ W, const TM* __restrict__ X, int K, int N_
     rslot = (rslot + 1 == NST) ? 0 : rslot + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail pieces retired before exit
+
+  if constexpr (EPI != EPI_BIAS_GELU_SPLIT) {
+    __syncthreads();                                 // every wave done with the ring
+    char* vs = ring + wave * 8192;
+    if constexpr (EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_F32)
+      staged_epilogue_f32<EPI, MT>(vs, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64, N_real, T_real,
+                                   bias, resid, out_f, ldo, oscale);
+    else
+      staged_epilogue_h<TM, EPI == EPI_BIAS_GELU, MT>(vs, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64,
+                                                      N_real, T_real, bias, out_h, ldo, oscale);
+    return;
+  }
 
   // epilogue: lane holds features f..f+3 of token t for each (m, n) block
 #pragma unroll
@@ -410,58 +517,12 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     return;
   }
 
-  // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well: per chunk of 2 row
-  // blocks a wave stages 32 features x 64 tokens (8 KiB, 16-B granules XOR-swizzled by token)
-  // and writes -- reading the residual alongside -- 128-B row pieces (from the accumulators
-  // each store covered 64 B of 16 rows)
+  // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well
   else {
-  static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
-  __syncthreads();                                 // every wave done with the ring
-  char* vs = ring + wave * 8192;
-#pragma unroll
-  for (int c = 0; c < MT / 2; ++c) {
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int m = 2 * c + mi;
-      const int fl = mi * 16 + (lane >> 4) * 4;                 // feature within the 32
-      const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * (FT / 2) + c * 32 + fl);
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) {
-        const int tl = n * 16 + (lane & 15);
-        const float4 v = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
-                          fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
-        *reinterpret_cast<float4*>(vs + tl * 128 + (((fl >> 2) ^ (tl & 7)) << 4)) = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int gr = lane & 7;
-    const int fcol = f0 + wm * (FT / 2) + c * 32 + gr * 4;
-    // the 8 rows' residual pieces loaded together (one wait), then add + store
-    float4 rr[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int t = t0 + wn * 64 + i * 8 + (lane >> 3);
-      rr[i] = float4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (EPI == EPI_BIAS_RESID)   // clamped into the matrix: unconditional loads
-        rr[i] = *reinterpret_cast<const float4*>(resid + (size_t)min(t, T_real - 1) * ldo +
-                                                 min(fcol, N_real - 4));
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int tl = i * 8 + (lane >> 3);
-      const int t = t0 + wn * 64 + tl;
-      float4 v = *reinterpret_cast<const float4*>(vs + tl * 128 + ((gr ^ (tl & 7)) << 4));
-      if (t < T_real && fcol < N_real) {
-        v.x += rr[i].x; v.y += rr[i].y; v.z += rr[i].z; v.w += rr[i].w;
-        *reinterpret_cast<float4*>(out_f + (size_t)t * ldo + fcol) = v;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
+    __syncthreads();                               // every wave done with the ring
+    staged_epilogue_f32<EPI, MT>(ring + wave * 8192, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64,
+                                 N_real, T_real, bias, resid, out_f, ldo, oscale);
   }
 }
 
