@@ -633,7 +633,10 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
-static constexpr int kSampleStrideMax = 64;      // ... of the MAXONLY pre-pass (r01d)
+static constexpr int kSampleStrideMax = 128;     // ... of the MAXONLY pre-pass (r01d: 64; r02
+                                                  // with QW: 128 saves 0.13 ms per 10M x 768
+                                                  // search, the seed at global rank ~1000 instead
+                                                  // of ~600 adds no measurable appends)
 static constexpr int kPrepassMinTilesPerWg = 4;   // ... when each dense workgroup has >= 4 tiles
                                                   // (r01g, configs[1] 1M x 384 B = 256: 15 tiles
                                                   // per workgroup; seeded 0.32 ms vs cold 1.84 ms)
