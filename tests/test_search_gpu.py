@@ -334,9 +334,9 @@ def test_batch_sizes_both_kernels(hc, dtype, B):
 @pytest.mark.parametrize("B", [17, 200, 256])
 @pytest.mark.parametrize("variant", ["unit", "raw", "masked"])
 def test_query_stationary_kernels(hc, D, B, variant):
-    """The query-stationary kernel (17-256 queries): 1 query block per wave on 256-row tiles
-    (any B at KS = 4..24; B > 128 as two workgroups per partition when D > 384) and 2 blocks
-    per wave on 128-row tiles (B > 128, D <= 384).  Normalised rows (UNIT epilogue), raw rows
+    """The query-stationary kernels (17-256 queries): QS with 1 query block per wave on 256-row
+    tiles (any B at KS = 4..24) and 2 blocks per wave on 128-row tiles (B > 128, D <= 384); at
+    D = 768 a normalised corpus with B > 128 goes to QW (256 queries per workgroup).  Normalised rows (UNIT epilogue), raw rows
     (inverse norms from LDS; at D = 768 routed to v3/v4), a row mask; N not a multiple of the
     tile (last tile partly past the corpus end) and large enough for several tiles per
     workgroup (candidate compactions, the seeded pre-pass)."""
