@@ -633,10 +633,12 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
-static constexpr int kSampleStrideMax = 128;     // ... of the MAXONLY pre-pass (r01d: 64; r02
-                                                  // with QW: 128 saves 0.13 ms per 10M x 768
-                                                  // search, the seed at global rank ~1000 instead
-                                                  // of ~600 adds no measurable appends)
+static constexpr int kSampleStrideMax = 64;      // ... of the MAXONLY pre-pass (r01d), and
+static constexpr int kSampleStrideMaxLarge = 128; // from kLargeCorpusRows rows: the seed's global
+static constexpr int64_t kLargeCorpusRows = 4000000;  // rank ~1000 instead of ~600 is a smaller
+                                                  // fraction of a large corpus (r02: 10M x 768
+                                                  // B = 1024 -0.13 ms per search with 128; 1M x
+                                                  // 384 B = 256 +0.016 ms: 64 there)
 static constexpr int kPrepassMinTilesPerWg = 4;   // ... when each dense workgroup has >= 4 tiles
                                                   // (r01g, configs[1] 1M x 384 B = 256: 15 tiles
                                                   // per workgroup; seeded 0.32 ms vs cold 1.84 ms)
@@ -830,7 +832,9 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
       const bool maxonly = !th.prepass_topk && (wide || qs || qw);
       int stride = th.sample_stride > 0 ? th.sample_stride
-                                        : (maxonly ? kSampleStrideMax : kSampleStrideDefault);
+                                        : (maxonly ? (ix->n >= kLargeCorpusRows ? kSampleStrideMaxLarge
+                                                                                 : kSampleStrideMax)
+                                                   : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;
       // MAXONLY runs on the 256 x 256 kernel: nqpad / 256 query blocks, 256-row tiles (the
       // dense pass's tiles may be 128 rows: QS with two query blocks per wave)
