@@ -6,11 +6,11 @@
 export TMPDIR=/tmp
 T=tools/gpu_step.sh
 Q="python bench.py --encoder none --no-cpu-baseline --no-configs0 --sweep ,"
-$T r02e_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider && \
-$T r02e_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" && \
-$T r02e_bench 600 python bench.py && \
-$T r02e_kt 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02e_prof_kt -o run -- $Q --steps 10 --warmup 2 && \
-$T r02e_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/r02e_prof_fetch -o run -- $Q --steps 3 --warmup 1 && \
-$T r02e_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/r02e_prof_write -o run -- $Q --steps 3 --warmup 1 && \
-$T r02e_sq 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/r02e_prof_sq -o run -- $Q --steps 3 --warmup 1 && \
+$T r02f_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider && \
+$T r02f_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" && \
+$T r02f_bench 600 python bench.py && \
+$T r02f_kt 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r02f_prof_kt -o run -- $Q --steps 10 --warmup 2 && \
+$T r02f_fetch 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/r02f_prof_fetch -o run -- $Q --steps 3 --warmup 1 && \
+$T r02f_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/r02f_prof_write -o run -- $Q --steps 3 --warmup 1 && \
+$T r02f_sq 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/r02f_prof_sq -o run -- $Q --steps 3 --warmup 1 && \
 echo ALLDONE
