@@ -96,6 +96,14 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_cores():
+    """Host threads the CPU legs actually ran on: the BLAS / OpenMP thread count, capped by the
+    CPUs this process may run on (sched_getaffinity; the box's machine-wide count is larger)."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
+    return min(aff, int(env)) if env and env.isdigit() and int(env) > 0 else aff
+
+
 def make_shard(ix, hc, r0, r1, dim, dtype, dev, seed=1000, chunk=1 << 20):
     """Rows [r0, r1) of a deterministic global corpus (identical for any GPU count):
     global chunk c (1M rows) is N(0,1) from a Philox stream seeded (seed + c)."""
@@ -183,11 +191,10 @@ def cpu_baseline(E_rows_f16, Q, k, n_total):
     np.take_along_axis(s32, part, axis=1).argsort(axis=1)
     tt = time.perf_counter() - t1
     del s32, E32
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
-                  or os.cpu_count() or 1)
-    return {"value": qps, "unit": "queries/s", "cores": threads, "kind": "port",
+    return {"value": qps, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
             "cpu_model": cpu_model(), "threads_env": {v: os.environ.get(v) for v in (
                 "OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")},
+            "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"{nq} queries x {nr:,}-row slice of the same corpus (fp16 decoded to fp64), "
                       f"cosine_similarity fp64 + argsort[::-1][:{k}] in {t:.2f} s, "
                       f"extrapolated linearly to {n_total:,} rows",
@@ -336,7 +343,7 @@ def configs0_leg(hc):
                for g, c in zip(gpu_res, cpu_res))
     dmax = max(abs(x["similarity_score"] - sc) for g, c in zip(gpu_res, cpu_res)
                for x, (_, sc) in zip(g, c))
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads = cpu_cores()
     return {"workload": "configs[0]: data/Product*.csv (441 graph_builder.py documents) -> "
                         "MiniLM-shape encoder (seeded) -> vector top-5, threshold 0.3, 4 queries "
                         "(experiments/main.py:1179-1184)",

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -58,8 +59,10 @@ struct hcr_index {
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
       w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
-  DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again;
+  DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
+      f_hcnt, f_hmin;
   hcr_search_stats stats{};
+  int opt_qw1 = -1;             // HCR_OPT_QW1
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -131,7 +134,8 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax, &ix->w_sk,
                    &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
-                   &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again};
+                   &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
+                   &ix->f_hcnt, &ix->f_hmin};
   for (DevBuf* b : all) b->release();
   if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
@@ -314,6 +318,10 @@ extern "C" int hcr_index_dtype(const hcr_index* ix) { return ix ? ix->dtype : -1
 extern "C" int hcr_index_set_id_offset(hcr_index* ix, int64_t off) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   if (off < 0) return set_err(HCR_EINVAL, "negative id offset");
+  // once an id map exists the rows already in it keep the ids they were given; a new offset
+  // would apply only to later plain adds -- two numbering rules in one index, so refused
+  if (ix->has_idmap && off != ix->id_offset)
+    return set_err(HCR_EINVAL, "id offset cannot change after hcr_index_add_ids (ids are explicit)");
   ix->id_offset = off;
   return HCR_OK;
 }
@@ -397,6 +405,18 @@ extern "C" int hcr_index_set_timing(hcr_index* ix, int enable) {
   return HCR_OK;
 }
 
+extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  switch (option) {
+    case HCR_OPT_QW1:
+      if (value < -1 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 2]", value);
+      ix->opt_qw1 = value;
+      return HCR_OK;
+    default:
+      return set_err(HCR_EINVAL, "unknown index option %d", option);
+  }
+}
+
 extern "C" int hcr_index_last_stats(const hcr_index* ix, hcr_search_stats* out) {
   if (!ix || !out) return set_err(HCR_EINVAL, "NULL argument");
   *out = ix->stats;
@@ -411,6 +431,7 @@ static constexpr int kMaxKprime = 512;
 static constexpr int kMergeMaxKeys = 16384;     // keys per merge_lists_kernel block (128 KiB of
                                                 // LDS): one level for P x k' <= 256 x 64
 static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
+static constexpr int kMaxDevices = 64;          // per-device once-only kernel attributes
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
 
@@ -451,10 +472,12 @@ static constexpr int64_t kQ64WideMaxElems = 1500000000;   // rows x ld, see v3_c
 //   HCRAG_PREPASS_TOPK      the top-k' pre-pass form instead of MAXONLY
 //   HCRAG_QS_MAX            largest batch on the query-stationary kernel (0: off)
 //   HCRAG_QW_MIN            smallest batch on the wide query-stationary kernel
+//   HCRAG_QW1               default of HCR_OPT_QW1 (one-wave-per-SIMD large-batch kernel)
 struct TestHooks {
   int64_t q64_elems = kQ64WideMaxElems;
   int qs_max = 256;
   int qw_min = 0;                    // 0: the measured default (v3_cfg)
+  int qw1 = -1;                      // HCR_OPT_QW1 default (-1: the heuristic)
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
@@ -464,6 +487,7 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
     if (const char* e = getenv("HCRAG_QS_MAX")) t.qs_max = atoi(e);
     if (const char* e = getenv("HCRAG_QW_MIN")) t.qw_min = std::max(1, atoi(e));
+    if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(2, std::max(-1, atoi(e)));
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
@@ -475,10 +499,12 @@ static const TestHooks& hooks() {
   return h;
 }
 
-// qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h)
-struct V3Cfg { int rt, qt, nst; bool qs, qw = false; };
-// qw_ok: a UNIT corpus without a row mask and k' small enough for the QW candidate buffers
-static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok) {
+// qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h); qw1: the
+// one-wave-per-SIMD form (score_qw1.h), spread = its DMA issue spread over the MFMA groups
+struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false; };
+// qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
+// QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1
+static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
@@ -486,6 +512,14 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok) {
   // B = 256 3.73 vs 4.61); at D = 384 QS and QW tie at 129-256 (1M x 384, B = 256: 0.283 vs
   // 0.282 ms), so QW from 257 there.
   const int qw_from = hooks().qw_min > 0 ? hooks().qw_min : (ld / V3_BK >= 24 ? 129 : 257);
+  // QW1: 64 (D = 768) / 48 (D = 1024) queries per wave at one wave per SIMD.  D = 1024 has no
+  // other query-stationary kernel (256 queries x 1024 do not fit QW's waves), so it takes QW1
+  // from 257 queries by default; D = 768 only when asked (HCR_OPT_QW1).
+  if (opt_qw1 != 0 && unit_ok && qw1_ok && qw1_supported(ld)) {
+    const bool d1024 = ld / V3_BK == 32;
+    if ((opt_qw1 > 0 || d1024) && nq >= (d1024 ? 257 : qw_from))
+      return {qw1_rows(ld), qw1_queries(ld), 0, false, false, true, opt_qw1 != 2};
+  }
   if (nq >= qw_from && unit_ok && qw_ok && qw_supported(ld))
     return {qw_rows(ld), kQwQueries, kQwStages, false, true};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
@@ -514,7 +548,7 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok) {
 // the tile-slot rings (inverse norms, mask words, global bounds) need a tile's slot to
 // outlive NST-1 stages of look-ahead
 static bool v3_fits(const hcr_index* ix, V3Cfg c) {
-  if (c.qs || c.qw) return true;                  // QS sizes its own slot rings (QsLayout::NIS)
+  if (c.qs || c.qw || c.qw1) return true;         // QS sizes its own slot rings (QsLayout::NIS)
   return (V3_NIS - 1) * (ix->ld / V3_BK) > c.nst - 1;
 }
 
@@ -551,6 +585,30 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
            c.qt == 256 ? 2 : 1};
   return launch_qs(ix->dtype, q, st);
+}
+
+static int launch_qw1_ix(hcr_index* ix, V3Launch a, int cap, bool spread, hipStream_t st) {
+  QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
+           a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
+  return launch_qw1(ix->dtype, q, spread, st);
+}
+
+// Row partitions of a QW1 launch (one workgroup per CU, LDS-bound): the smallest P >= 256 / nqb
+// whose nqb x P workgroups fill their last round of 256 CUs to >= 97 % (nq = 8192 at D = 1024:
+// 43 query blocks x 29 partitions = 1247 workgroups in 5 rounds), else the best fill up to 256.
+static int qw1_partitions(int nqb, int ntiles) {
+  constexpr int kCus = 256;
+  const int p0 = std::max(1, kCus / nqb);
+  int best = p0;
+  double best_fill = 0.0;
+  for (int P = p0; P <= std::max(p0, std::min(256, ntiles)); ++P) {
+    const int64_t nwg = (int64_t)nqb * P;
+    const double fill = (double)nwg / (double)(((nwg + kCus - 1) / kCus) * kCus);
+    if (fill >= 0.97) return P;
+    if (fill > best_fill + 1e-9) { best_fill = fill; best = P; }
+  }
+  return best;
 }
 
 static int launch_qw_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
@@ -611,6 +669,7 @@ template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
   if (c.qs) return launch_qs_ix(ix, c, a, st);              // CAP chosen in score_qs.hip
   if (c.qw) return launch_qw_ix(ix, a, cap, st);
+  if (c.qw1) return launch_qw1_ix(ix, a, cap, c.spread, st);
   switch (cap) {
     case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
     case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
@@ -684,12 +743,16 @@ seed_from_maxima_kernel(const float* __restrict__ umax, int U, int nqpad, int j,
 static int merge_groups(int kp) { return std::min(256, std::max(2, kMergeMaxKeys / kp)); }
 static int merge_lists(hcr_index* ix, int nq, int nqpad, int P, int kp, hipStream_t st,
                        const uint64_t** out) {
-  static bool lds_set = false;
-  if (!lds_set) {
-    HIPC(hipFuncSetAttribute((const void*)merge_lists_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, kMergeMaxKeys * 8));
-    lds_set = true;
-  }
+  // the dynamic-LDS limit is a per-device attribute: raised once per device, by whichever
+  // thread gets there first (hcr_multi_search runs shards of several devices concurrently)
+  static std::once_flag lds_once[kMaxDevices];
+  if (ix->device < 0 || ix->device >= kMaxDevices) return set_err(HCR_EINVAL, "device %d", ix->device);
+  hipError_t lds_err = hipSuccess;
+  std::call_once(lds_once[ix->device], [&] {
+    lds_err = hipFuncSetAttribute((const void*)merge_lists_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kMergeMaxKeys * 8);
+  });
+  HIPC(lds_err);
   const int G = merge_groups(kp);
   const int P2 = (P + G - 1) / G;
   const uint64_t* src = ix->w_part.as<const uint64_t>();
@@ -751,19 +814,23 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     memcpy(&ix->unit_dev_host, &ud_bits, 8);
     ix->rho_dirty = false;
   }
+  const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
-                          !ix->has_mask && ix->dtype != HCR_F32 && qw_cap(kp, ix->ld) > 0);
+                          qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
+                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
-  const bool qs = ver == 3 && c3.qs, qw = ver == 3 && c3.qw;
+  const bool qs = ver == 3 && c3.qs, qw = ver == 3 && c3.qw, qw1 = ver == 3 && c3.qw1;
   // QS batches are padded to 256 queries for their MAXONLY pre-pass on the 256 x 256 kernel
-  const int nqpad = (int)round_up(nq, qs ? 256 : tq);
+  // (QW1's 192-query blocks: to both)
+  const int nqpad = (int)(qw1 ? round_up(round_up(nq, tq), 256) : round_up(nq, qs ? 256 : tq));
   const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
-  const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : next_pow2(kp + tr);
+  const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : qw1 ? qw1_cap(kp, ix->ld) : next_pow2(kp + tr);
   const int wg_target = ver == 1 ? 512 : 256;
   // (QW: one workgroup per CU -- its LDS -- so at most 256 workgroups: one round)
-  int P = qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
+  int P = qw1 ? qw1_partitions(nqb, ntiles)
+               : qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
   const bool tm_f16 = ix->dtype == HCR_F16;
@@ -795,10 +862,11 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
   const bool wide = ver == 3 && c3.rt == 256 && c3.qt == 256;   // v4
-  const bool unit = (wide || qs || qw) && ix->unit_dev_host <= kUnitDevMax;
+  const bool unit = (wide || qs || qw || qw1) && ix->unit_dev_host <= kUnitDevMax;
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
-  if (ix->stats.score_kernel == 0) ix->stats.score_kernel = ver == 1 ? 1 : qw ? 6 : qs ? 5 : wide ? 4 : 3;
+  if (ix->stats.score_kernel == 0)
+    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? 7 : qw ? 6 : qs ? 5 : wide ? 4 : 3;
 
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)
@@ -830,7 +898,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // Two pre-pass forms: MAXONLY (default for the 256 x 256 kernel: the largest score of
       // every sampled 128-row unit per query, no candidate lists, stride 64) and the top-k'
       // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
-      const bool maxonly = !th.prepass_topk && (wide || qs || qw);
+      const bool maxonly = !th.prepass_topk && (wide || qs || qw || qw1);
       int stride = th.sample_stride > 0 ? th.sample_stride
                                         : (maxonly ? (ix->n >= kLargeCorpusRows ? kSampleStrideMaxLarge
                                                                                  : kSampleStrideMax)
@@ -913,7 +981,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
 
 // ---- exact fallback (K6 + K7, topk_kernels.h) ----
 static constexpr int kFallbackCap = 8192;     // buffer slots per query (LDS sort of 2 x 64 KiB)
-static constexpr int kFallbackGroup = 32;     // queries per row scan
+static constexpr int kFallbackGroup = kFbGroup;  // queries per row scan (K6's LDS histograms)
 static constexpr int kFallbackMaxRounds = 64; // each round strictly raises the threshold key
 static constexpr int kMaxFastK = 256;         // k' = 2k <= 512: larger k go straight to K6/K7
 static constexpr int kMaxK = 2048;            // kFallbackCap > k: every K7 round makes progress
@@ -940,8 +1008,24 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     CHECK(ix->f_bufh.ensure((size_t)ng * cap * 8));
     CHECK(ix->f_bufl.ensure((size_t)ng * cap * 8));
     CHECK(ix->f_again.ensure(16));
+    CHECK(ix->f_hlo.ensure((size_t)ng * 8));
+    CHECK(ix->f_hhi.ensure((size_t)ng * 8));
+    CHECK(ix->f_hcnt.ensure((size_t)ng * (kFbBins + 1) * 4));
+    CHECK(ix->f_hmin.ensure((size_t)ng * (kFbBins + 1) * 8));
     std::vector<uint64_t> thh(sk.begin() + g0, sk.begin() + g0 + ng), thl(ng, 0ull);
     std::vector<int> act(ng, 1);
+    // histogram range of the first round: [score of the starting threshold, just above 1]
+    std::vector<double> hlo(ng), hhi(ng, 1.0 + 1e-6);
+    for (int i = 0; i < ng; ++i) {
+      if (thh[i] == 0ull) { hlo[i] = -1.0 - 1e-6; continue; }
+      const uint64_t u = thh[i];
+      const uint64_t b = (u & 0x8000000000000000ull) ? (u ^ 0x8000000000000000ull) : ~u;
+      double v;
+      memcpy(&v, &b, 8);
+      hlo[i] = v;
+    }
+    HIPC(hipMemcpyAsync(ix->f_hlo.p, hlo.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(ix->f_hhi.p, hhi.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(ix->f_idx.p, idx.data() + g0, (size_t)ng * 4, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(ix->f_thl.p, thl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
@@ -951,13 +1035,16 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
                        ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
     HIPC(hipGetLastError());
-    const unsigned fgrid = (unsigned)std::min<int64_t>((ix->n + 3) / 4, 8192);
+    // (one histogram flush per block: 2048 blocks x 4 waves, ~1.2k rows per wave at 10M rows)
+    const unsigned fgrid = (unsigned)std::min<int64_t>((ix->n + 3) / 4, 2048);
     int again = 1, rounds = 0;
     while (again > 0) {
       if (++rounds > kFallbackMaxRounds)
         return set_err(HCR_EHIP, "internal: exact fallback did not converge in %d rounds", kFallbackMaxRounds);
       HIPC(hipMemsetAsync(ix->f_cnt.p, 0, (size_t)ng * 4, st));
       HIPC(hipMemsetAsync(ix->f_again.p, 0, 4, st));
+      HIPC(hipMemsetAsync(ix->f_hcnt.p, 0, (size_t)ng * (kFbBins + 1) * 4, st));
+      HIPC(hipMemsetAsync(ix->f_hmin.p, 0xFF, (size_t)ng * (kFbBins + 1) * 8, st));
 #define FIL(TS)                                                                                  \
   hipLaunchKernelGGL((exact_filter_kernel<TS>), dim3(fgrid), dim3(256), 0, st,                  \
                      ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<const double>(),       \
@@ -965,7 +1052,9 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,                \
                      ix->f_thh.as<const uint64_t>(), ix->f_thl.as<const uint64_t>(),            \
                      ix->f_act.as<const int>(), cap, ix->f_cnt.as<unsigned int>(),               \
-                     ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>())
+                     ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
+                     ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
+                     ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>())
       if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
 #undef FIL
       hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
@@ -973,7 +1062,9 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                          ix->f_bufl.as<const uint64_t>(), ix->f_thh.as<uint64_t>(),
                          ix->f_thl.as<uint64_t>(), ix->f_act.as<int>(), ix->f_again.as<int>(), mode,
                          thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
-                         ix->f_idx.as<const int>(), os, oi);
+                         ix->f_idx.as<const int>(), os, oi, ix->f_hlo.as<double>(),
+                         ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
+                         ix->f_hmin.as<const unsigned long long>());
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&again, ix->f_again.p, 4, hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));

@@ -6,9 +6,10 @@
 // them use every GPU of a node without torchrun.  Rows are sharded in contiguous blocks over
 // the listed devices (a device may be listed more than once: several shards on one GPU), each
 // shard is an ordinary hcr_index with its own stream, searched from its own host thread; the
-// shards' exact top-k lists are exchanged to the first device -- RCCL all-gather
-// (ncclCommInitAll over the distinct devices, one communicator per device) or, when devices
-// repeat or RCCL cannot be loaded, peer copies -- and merged there by K5 (merge_shards_kernel).
+// shards' exact top-k lists are gathered on the first device -- RCCL point-to-point sends to
+// it (ncclCommInitAll over the distinct devices, one communicator per device; only the merging
+// device receives) or, when devices repeat, RCCL cannot be loaded or its communicators cannot be
+// created, peer copies -- and merged there by K5 (merge_shards_kernel).
 //
 // RCCL is bound at run time (dlopen of librccl.so.1): a process that already holds PyTorch's
 // RCCL (same SONAME) shares that one instead of loading a second copy.
@@ -32,7 +33,8 @@ struct Rccl {
   bool tried = false, ok = false;
   ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
-  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*group_start)() = nullptr;
   ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
@@ -47,11 +49,12 @@ Rccl& rccl() {
   if (!h) return r;
   r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
   r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
-  r.all_gather = reinterpret_cast<decltype(r.all_gather)>(dlsym(h, "ncclAllGather"));
+  r.send = reinterpret_cast<decltype(r.send)>(dlsym(h, "ncclSend"));
+  r.recv = reinterpret_cast<decltype(r.recv)>(dlsym(h, "ncclRecv"));
   r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
   r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-  r.ok = r.comm_init_all && r.comm_destroy && r.all_gather && r.group_start && r.group_end &&
+  r.ok = r.comm_init_all && r.comm_destroy && r.send && r.recv && r.group_start && r.group_end &&
          r.error_string;
   return r;
 }
@@ -72,7 +75,6 @@ struct hcr_multi_shard {
   hcr_index* ix = nullptr;
   hipStream_t st = nullptr;
   DevBuf q, s, i;                     // queries and this shard's [nq][k] exact lists
-  DevBuf gs, gi;                      // RCCL receive buffers [g][nq][k]
   std::vector<int64_t> gids;          // global id of each local row (host copy, for masks)
 };
 
@@ -82,7 +84,8 @@ struct hcr_multi_index {
   std::vector<hcr_multi_shard> sh;
   bool distinct = false;              // every shard on its own device
   bool rccl_init = false;
-  int exchange = 0;                   // 1: RCCL all-gather, 0: peer / device copies
+  int exchange = 0;                   // 1: RCCL gather to shard 0, 0: peer / device copies
+  DevBuf gs, gi;                      // on shard 0's device: the merge's second ping-pong pair
   std::vector<ncclComm_t> comms;
   DevBuf cs, ci, ms, mi;              // on shard 0's device: gathered lists, merged lists
   hcr_search_stats stats{};
@@ -125,13 +128,13 @@ extern "C" int hcr_multi_destroy(hcr_multi_index* m) {
   for (auto& s : m->sh) {
     (void)hipSetDevice(s.dev);
     if (s.st) (void)hipStreamSynchronize(s.st);
-    s.q.release(); s.s.release(); s.i.release(); s.gs.release(); s.gi.release();
+    s.q.release(); s.s.release(); s.i.release();
     if (s.st) (void)hipStreamDestroy(s.st);
     if (s.ix) hcr_index_destroy(s.ix);
   }
   if (!m->sh.empty()) {
     (void)hipSetDevice(m->sh[0].dev);
-    m->cs.release(); m->ci.release(); m->ms.release(); m->mi.release();
+    m->cs.release(); m->ci.release(); m->ms.release(); m->mi.release(); m->gs.release(); m->gi.release();
   }
   delete m;
   return HCR_OK;
@@ -164,7 +167,10 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
     const int rc = hcr_index_add_ids(s.ix, (const char*)rows + (size_t)r0 * rb, r1 - r0, rows_dtype,
                                      normalize, s.gids.data() + old);
     if (rc != HCR_OK) {
+      // shards 0..j-1 already hold their blocks under ids m->n + r: the call's ids are
+      // consumed (never handed out again), the failed blocks are simply absent
       s.gids.resize(old);
+      m->n += n;
       return rc;
     }
   }
@@ -196,7 +202,11 @@ static int init_rccl(hcr_multi_index* m) {
   std::vector<int> devs(m->g);
   for (int j = 0; j < m->g; ++j) devs[j] = m->sh[j].dev;
   m->comms.assign(m->g, nullptr);
-  NCCLC(rccl().comm_init_all(m->comms.data(), m->g, devs.data()));
+  // a node whose RCCL cannot build communicators still searches, on peer copies
+  if (rccl().comm_init_all(m->comms.data(), m->g, devs.data()) != ncclSuccess) {
+    m->comms.clear();
+    return HCR_OK;
+  }
   m->exchange = 1;
   return HCR_OK;
 }
@@ -248,42 +258,38 @@ extern "C" int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_
     m->stats.workgroups += st.workgroups;
     m->stats.score_kernel = std::max(m->stats.score_kernel, st.score_kernel);
   }
-  // 2) exchange: every shard's lists to shard 0's device as [g][nq][k]
+  // 2) exchange: every shard's lists to shard 0's device as [g][nq][k] in m->cs / m->ci
   hcr_multi_shard& s0 = m->sh[0];
-  double* S;
-  int64_t* I;
+  HIPC(hipSetDevice(s0.dev));
+  CHECK(m->cs.ensure(lst * g * 8));
+  CHECK(m->ci.ensure(lst * g * 8));
+  double* S = m->cs.as<double>();
+  int64_t* I = m->ci.as<int64_t>();
+  HIPC(hipMemcpyAsync(S, s0.s.p, lst * 8, hipMemcpyDeviceToDevice, s0.st));
+  HIPC(hipMemcpyAsync(I, s0.i.p, lst * 8, hipMemcpyDeviceToDevice, s0.st));
   if (m->exchange == 1) {
-    for (auto& s : m->sh) {
-      HIPC(hipSetDevice(s.dev));
-      CHECK(s.gs.ensure(lst * g * 8));
-      CHECK(s.gi.ensure(lst * g * 8));
-    }
+    // a gather, not an all-gather: only the merging device receives (g - 1 lists of
+    // nq x k x 16 bytes over its xGMI links)
     NCCLC(rccl().group_start());
-    for (auto& s : m->sh) {
-      NCCLC(rccl().all_gather(s.s.p, s.gs.p, lst, ncclFloat64, m->comms[&s - m->sh.data()], s.st));
-      NCCLC(rccl().all_gather(s.i.p, s.gi.p, lst, ncclInt64, m->comms[&s - m->sh.data()], s.st));
+    for (int j = 1; j < g; ++j) {
+      hcr_multi_shard& s = m->sh[j];
+      NCCLC(rccl().send(s.s.p, lst, ncclFloat64, 0, m->comms[j], s.st));
+      NCCLC(rccl().send(s.i.p, lst, ncclInt64, 0, m->comms[j], s.st));
+      NCCLC(rccl().recv(S + (size_t)j * lst, lst, ncclFloat64, j, m->comms[0], s0.st));
+      NCCLC(rccl().recv(I + (size_t)j * lst, lst, ncclInt64, j, m->comms[0], s0.st));
     }
     NCCLC(rccl().group_end());
-    for (auto& s : m->sh) {
-      HIPC(hipSetDevice(s.dev));
-      HIPC(hipStreamSynchronize(s.st));
+    for (int j = 1; j < g; ++j) {
+      HIPC(hipSetDevice(m->sh[j].dev));
+      HIPC(hipStreamSynchronize(m->sh[j].st));
     }
     HIPC(hipSetDevice(s0.dev));
-    CHECK(m->cs.ensure(lst * g * 8));                // merge ping-pong buffer
-    CHECK(m->ci.ensure(lst * g * 8));
-    S = s0.gs.as<double>();
-    I = s0.gi.as<int64_t>();
   } else {
-    HIPC(hipSetDevice(s0.dev));
-    CHECK(m->cs.ensure(lst * g * 8));
-    CHECK(m->ci.ensure(lst * g * 8));
-    for (int j = 0; j < g; ++j) {
+    for (int j = 1; j < g; ++j) {
       const hcr_multi_shard& s = m->sh[j];
-      HIPC(hipMemcpyPeerAsync(m->cs.as<double>() + (size_t)j * lst, s0.dev, s.s.p, s.dev, lst * 8, s0.st));
-      HIPC(hipMemcpyPeerAsync(m->ci.as<int64_t>() + (size_t)j * lst, s0.dev, s.i.p, s.dev, lst * 8, s0.st));
+      HIPC(hipMemcpyPeerAsync(S + (size_t)j * lst, s0.dev, s.s.p, s.dev, lst * 8, s0.st));
+      HIPC(hipMemcpyPeerAsync(I + (size_t)j * lst, s0.dev, s.i.p, s.dev, lst * 8, s0.st));
     }
-    S = m->cs.as<double>();
-    I = m->ci.as<int64_t>();
   }
   // 3) K5 merge on shard 0's device, in rounds of at most kMergeMaxKeys / k lists
   CHECK(m->ms.ensure(lst * g * 8));
@@ -293,14 +299,10 @@ extern "C" int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_
   const int64_t* src_i = I;
   const int G = std::max(1, kMergeMaxKeys / k);
   bool into_m = true;
-  double* bs[2] = {m->ms.as<double>(), m->cs.as<double>()};
-  int64_t* bi[2] = {m->mi.as<int64_t>(), m->ci.as<int64_t>()};
-  if (m->exchange == 0) {                       // cs/ci hold the gathered lists: use s0.gs/gi
-    CHECK(s0.gs.ensure(lst * g * 8));
-    CHECK(s0.gi.ensure(lst * g * 8));
-    bs[1] = s0.gs.as<double>();
-    bi[1] = s0.gi.as<int64_t>();
-  }
+  CHECK(m->gs.ensure(lst * g * 8));             // cs / ci hold the gathered lists
+  CHECK(m->gi.ensure(lst * g * 8));
+  double* bs[2] = {m->ms.as<double>(), m->gs.as<double>()};
+  int64_t* bi[2] = {m->mi.as<int64_t>(), m->gi.as<int64_t>()};
   while (lists > 1) {
     const int groups = (lists + G - 1) / G;
     double* ds = bs[into_m ? 0 : 1];

@@ -39,3 +39,11 @@ int qw_cap(int kp, int ld);           // candidate buffer slots per query (0: k'
 int launch_qw(int dtype, const QsArgs& a, hipStream_t st);
 constexpr int kQwQueries = 256;       // queries per QW workgroup (= QW_QT)
 constexpr int kQwStages = 3;          // QW ring stages (= QW_NST)
+
+// One-wave-per-SIMD query-stationary kernel (score_qw1.h): 256 (D = 768) or 192 (D = 1024)
+// queries per workgroup, UNIT corpora without a row mask.
+bool qw1_supported(int ld);
+int qw1_rows(int ld);                 // rows per stage (the kernel's row tile)
+int qw1_queries(int ld);              // queries per workgroup
+int qw1_cap(int kp, int ld);          // candidate buffer slots per query (0: k' too large)
+int launch_qw1(int dtype, const QsArgs& a, bool spread, hipStream_t st);

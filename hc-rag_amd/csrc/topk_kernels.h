@@ -703,16 +703,26 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
 
 // -------------------------------------------------------------------------------------
 // K6/K7: exact fallback (queries the certificate could not settle at k' = 512, and k > 256).
-//   K6 scans every row once for a group of queries: fp64 cosine in the same summation order
-//   as K4 (so the scores are bit-identical), and appends each row whose key (score desc, row
-//   asc) is >= the query's threshold key to a per-query buffer of `cap` slots.
+//   K6 scans every row once for a group of <= kFbGroup queries: fp64 cosine in the same
+//   summation order as K4 (so the scores are bit-identical), and appends each row whose key
+//   (score desc, row asc) is >= the query's threshold key to a per-query buffer of `cap` slots.
+//   Beside it, every admitted row lands in a per-query histogram: kFbBins bins linear in the
+//   score over [h_lo, h_hi) plus one bin for scores >= h_hi, each with its row count and the
+//   smallest score key it holds (LDS per block, flushed by atomics).
 //   K7 sorts a query's buffer in LDS.  If it did not overflow it holds every row at or above
 //   the threshold, which is <= the true k-th best key, so its top-k IS the exact top-k.  If it
-//   overflowed, the k-th best of the slots it kept is a tighter threshold (still <= the true
-//   k-th best, and strictly above the old one because cap > k and keys are unique): the host
-//   re-runs K6 for those queries.  Starting threshold: K4's s_k (the k-th best exact score
-//   among the candidates), or the lowest key.
+//   overflowed, the next threshold is the larger of
+//     (a) the smallest key among the top bins that together hold >= k rows: at least k rows
+//         score at or above it, whatever order the scan admitted them in, and the next round's
+//         histogram spans only the bin where the k-th best lies (a 1/kFbBins zoom per round);
+//     (b) the k-th best key of the slots it kept (strictly above the old threshold because
+//         cap > k and keys are unique: progress even through runs of identical scores),
+//   both <= the true k-th best key; the host re-runs K6 for those queries.  Starting
+//   threshold: K4's s_k (the k-th best exact score among the candidates), or the lowest key.
 // -------------------------------------------------------------------------------------
+constexpr int kFbGroup = 32;     // queries per K6 scan (the LDS histograms)
+constexpr int kFbBins = 128;     // linear score bins per query (+ 1 for scores >= h_hi)
+
 template <typename TS>
 __global__ void __launch_bounds__(256)
 exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
@@ -721,26 +731,53 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
                     const uint32_t* __restrict__ maskbits, const uint64_t* __restrict__ th_hi,
                     const uint64_t* __restrict__ th_lo, const int* __restrict__ active, int cap,
                     unsigned int* __restrict__ cnt, uint64_t* __restrict__ buf_hi,
-                    uint64_t* __restrict__ buf_lo) {
+                    uint64_t* __restrict__ buf_lo, const double* __restrict__ h_lo,
+                    const double* __restrict__ h_hi, unsigned int* __restrict__ h_cnt,
+                    unsigned long long* __restrict__ h_min) {
+  __shared__ unsigned int s_cnt[kFbGroup][kFbBins + 1];
+  __shared__ unsigned long long s_min[kFbGroup][kFbBins + 1];
+  for (int i = threadIdx.x; i < kFbGroup * (kFbBins + 1); i += blockDim.x) {
+    (&s_cnt[0][0])[i] = 0u;
+    (&s_min[0][0])[i] = ~0ull;
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const bool hoist = dim <= 1024;          // the row's first two 512-wide pieces in registers
   for (int64_t row = w0; row < n; row += nw) {
     if (maskbits && !((maskbits[row >> 5] >> (row & 31)) & 1u)) continue;
     const TS* e = rows + row * ld;
     const double nr = norm64[row];
+    float xr[2][8];
+    if (hoist) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int d0 = lane * 8 + 512 * c;
+        if (d0 < dim) load8_f32(e + d0, xr[c]);
+        else
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xr[c][j] = 0.f;
+      }
+    }
     for (int q = 0; q < nq; ++q) {
       if (!active[q]) continue;
       const float* qs = q32 + (int64_t)q * dim;
       double acc = 0.0;
-      for (int d0 = lane * 8; d0 < dim; d0 += 512) {
-        float x[8];
-        load8_f32(e + d0, x);
-        acc8_f64(acc, qs, d0, dim, x);
+      if (hoist) {
+        acc8_f64(acc, qs, lane * 8, dim, xr[0]);
+        acc8_f64(acc, qs, lane * 8 + 512, dim, xr[1]);
+      } else {
+        for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+          float x[8];
+          load8_f32(e + d0, x);
+          acc8_f64(acc, qs, d0, dim, x);
+        }
       }
       acc = wave_sum_f64(acc);
       if (lane == 0) {
-        const uint64_t h = ord64(acc / (qnorm[q] * nr));
+        const double sc = acc / (qnorm[q] * nr);
+        const uint64_t h = ord64(sc);
         const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)row);
         if (h > th_hi[q] || (h == th_hi[q] && l >= th_lo[q])) {
           const unsigned int p = atomicAdd(&cnt[q], 1u);
@@ -748,8 +785,24 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
             buf_hi[(size_t)q * cap + p] = h;
             buf_lo[(size_t)q * cap + p] = l;
           }
+          const double lo = h_lo[q], hi = h_hi[q];
+          int b = kFbBins;
+          if (sc < hi) {
+            const double t = (sc - lo) * ((double)kFbBins / (hi - lo));
+            b = t < 0.0 ? 0 : t >= (double)(kFbBins - 1) ? kFbBins - 1 : (int)t;
+          }
+          atomicAdd(&s_cnt[q][b], 1u);
+          atomicMin(&s_min[q][b], (unsigned long long)h);
         }
       }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nq * (kFbBins + 1); i += blockDim.x) {
+    const unsigned int c = (&s_cnt[0][0])[i];
+    if (c) {
+      atomicAdd(&h_cnt[i], c);
+      atomicMin(&h_min[i], (&s_min[0][0])[i]);
     }
   }
 }
@@ -762,7 +815,9 @@ exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
                     int* __restrict__ active, int* __restrict__ n_again, int mode, double thr,
                     int64_t id_offset, const int64_t* __restrict__ idmap,
                     const int* __restrict__ out_idx, double* __restrict__ out_s,
-                    int64_t* __restrict__ out_i) {
+                    int64_t* __restrict__ out_i, double* __restrict__ h_lo,
+                    double* __restrict__ h_hi, const unsigned int* __restrict__ h_cnt,
+                    const unsigned long long* __restrict__ h_min) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm_sel[];
   const int q = blockIdx.x;
   if (!active[q]) return;
@@ -781,8 +836,30 @@ exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
   block_sort_desc_pair(hi, lo, m);
   if (c > (unsigned int)cap) {
     if (threadIdx.x == 0) {
-      th_hi[q] = hi[k - 1];
-      th_lo[q] = lo[k - 1];
+      // (a) the histogram: top bins down to the one where k rows are reached (the admitted
+      // rows number c > cap > k, so that bin exists)
+      const unsigned int* hc = h_cnt + (size_t)q * (kFbBins + 1);
+      const unsigned long long* hm = h_min + (size_t)q * (kFbBins + 1);
+      unsigned int acc = 0u;
+      unsigned long long mn = ~0ull;
+      int b = kFbBins;
+      for (; b >= 0; --b) {
+        acc += hc[b];
+        if (hc[b] && hm[b] < mn) mn = hm[b];
+        if (acc >= (unsigned int)k) break;
+      }
+      uint64_t nh = mn, nl = 0ull;
+      // (b) the k-th best of the kept slots
+      if (hi[k - 1] > nh || (hi[k - 1] == nh && lo[k - 1] > nl)) { nh = hi[k - 1]; nl = lo[k - 1]; }
+      const double olo = h_lo[q], ohi = h_hi[q];
+      const double nlo = unord64(nh);
+      // the k-th best lies in bin b (the bins above it hold < k rows): zoom there
+      double nhi = b >= kFbBins ? 2.0 : olo + (double)(b + 1) * ((ohi - olo) / (double)kFbBins);
+      if (!(nhi > nlo)) nhi = nextafter(nlo, INFINITY);
+      th_hi[q] = nh;
+      th_lo[q] = nl;
+      h_lo[q] = nlo;
+      h_hi[q] = nhi;
       atomicAdd(n_again, 1);
     }
     return;

@@ -178,12 +178,20 @@ class VectorIndex:
         """HIP-event timing of the fused score kernel (reported by ``last_stats``)."""
         check(lib().hcr_index_set_timing(self._h, 1 if enable else 0))
 
+    OPT_QW1 = 1
+
+    def set_option(self, option: int, value: int) -> None:
+        """Kernel-choice option (``hcr_index_set_option``); never changes results.
+        ``VectorIndex.OPT_QW1``: -1 heuristic, 0 never QW1, 1 QW1 (DMA spread), 2 QW1 (DMA at
+        the stage barrier)."""
+        check(lib().hcr_index_set_option(self._h, int(option), int(value)))
+
 
 class MultiDeviceIndex:
     """One process, several GPUs (``hcr_multi_*``): rows sharded in
     contiguous blocks over ``devices`` (a device may repeat), every shard searched concurrently,
-    per-shard exact top-k lists exchanged to ``devices[0]`` (RCCL all-gather over distinct
-    devices, peer copies otherwise) and merged there.  Same ``add`` / ``search`` /
+    per-shard exact top-k lists gathered on ``devices[0]`` (RCCL sends over distinct devices,
+    peer copies otherwise or when RCCL cannot create communicators) and merged there.  Same ``add`` / ``search`` /
     ``set_rowmask`` surface and results as ``VectorIndex`` over all rows."""
 
     def __init__(self, dim: int, devices, dtype: str = "f16", capacity: int = 0):

@@ -14,8 +14,15 @@ Replaces experiments/embedding_generator.py's ``DynamicEmbeddingGenerator`` inge
 The text representation follows :28-104 (field importance from avg length / unique ratio,
 "Table: name" then high / first 3 medium / first 2 low fields, joined by ". ") and the metadata
 :130-145 (``id``, ``type``, ``table_name``, ``row_index``, ``source_file``, ``entity_id`` from
-the first column whose name contains "id").  JSON documents follow :152-215.  PDF extraction
-(:218-364) needs pdfplumber / PyPDF2, absent here: out of scope.
+the first column whose name contains "id").  JSON documents follow :152-215 (the parent document
+from " Table " in the file name, :385-389).  PDF documents follow :278-364: the extracted text is
+cut by ``chunk_text`` (800 characters, 100 overlap, sentence-boundary search) and every chunk,
+prefixed "PDF Document: {name}. ", is encoded in ONE batched call (the reference: one encode per
+chunk, :326-337).  Text extraction itself (:218-276, pdfplumber / PyPDF2) is the caller's: pass
+``extract_text`` (a callable) or already-extracted ``text``; pdfplumber / PyPDF2 are used when
+importable, and otherwise the reference's own extraction-failure text is embedded (:270-272).
+Parity: tests/golden/make_ingest_f1.py restates these lines independently over the reference's
+data/ and its fixture pins texts, metadata and (CPU BertModel fp32) embeddings.
 """
 from __future__ import annotations
 
@@ -126,6 +133,61 @@ def flatten_json_to_text(obj, prefix: str = "") -> List[str]:
     else:
         out.append(f"{prefix}: {obj}" if prefix else str(obj))
     return out
+
+
+def chunk_text(text: str, max_chunk_size: int = 1000, overlap: int = 100) -> List[str]:
+    """embedding_generator.py:278-305: windows of max_chunk_size characters, each ended at the
+    last '.', '!' or '?' found scanning back from the window end (at most 200 characters and not
+    into the window's first half), the next window starting `overlap` characters before the
+    previous end -- including the reference's short trailing window when the last end overshoots
+    the text by less than `overlap`."""
+    n = len(text)
+    if n <= max_chunk_size:
+        return [text]
+    out: List[str] = []
+    start = 0
+    while start < n:
+        end = start + max_chunk_size
+        if end < n:
+            lo = max(start + max_chunk_size // 2, end - 200)
+            for i in range(end, lo, -1):
+                if text[i] in ".!?":
+                    end = i + 1
+                    break
+        piece = text[start:end].strip()
+        if piece:
+            out.append(piece)
+        start = end - overlap
+        if start >= n:
+            break
+    return out
+
+
+def extract_pdf_text(pdf_path) -> str:
+    """embedding_generator.py:218-276 when pdfplumber / PyPDF2 are importable ("Page n: ..."
+    lines; pdfplumber first, whitespace-collapsed); "" when neither reads the file."""
+    pages: List[str] = []
+    try:
+        import pdfplumber
+        with pdfplumber.open(pdf_path) as pdf:
+            for i, page in enumerate(pdf.pages):
+                t = page.extract_text()
+                if t and t.strip():
+                    pages.append(f"Page {i + 1}: " + " ".join(t.split()))
+    except Exception:
+        pages = []
+    if not "\n".join(pages).strip():
+        pages = []
+        try:
+            import PyPDF2
+            with open(pdf_path, "rb") as fh:
+                for i, page in enumerate(PyPDF2.PdfReader(fh).pages):
+                    t = page.extract_text()
+                    if t.strip():
+                        pages.append(f"Page {i + 1}: {t.strip()}")
+        except Exception:
+            pages = []
+    return "\n".join(pages)
 
 
 def read_csv_like_graph_builder(path):
@@ -240,13 +302,51 @@ class BatchedEmbeddingGenerator:
                                "json_keys": list(data.keys()) if isinstance(data, dict) else []}])
         return 1
 
-    def process_all_data(self, data_directory) -> None:
-        """CSV (';'-separated) and JSON files of a directory (PDFs: out of scope here)."""
+    def process_text_document(self, text: str, document_name: str, source_file: str = "",
+                              file_size: int = 0, max_chunk_size: int = 800,
+                              overlap: int = 100) -> int:
+        """embedding_generator.py:307-364 after text extraction: chunk_text, the
+        "PDF Document: {name}. " prefix and per-chunk metadata, all chunks in ONE encode call."""
+        if not text.strip():
+            return 0
+        chunks = chunk_text(text, max_chunk_size, overlap)
+        ctx = f"PDF Document: {document_name}. "
+        metas = [{"id": f"pdf_{document_name}_chunk_{j}", "type": "pdf_document",
+                  "document_name": document_name, "source_file": source_file, "chunk_index": j,
+                  "total_chunks": len(chunks), "text_length": len(c), "file_size": file_size}
+                 for j, c in enumerate(chunks)]
+        self._append([ctx + c for c in chunks], metas)
+        return len(chunks)
+
+    def process_pdf_document(self, pdf_path, document_name=None, text: Optional[str] = None,
+                             extract_text=None) -> int:
+        """embedding_generator.py:307-364.  The text is `text`, else `extract_text(pdf_path)`,
+        else extract_pdf_text (pdfplumber / PyPDF2 when importable); when none yields any,
+        the reference's extraction-failure sentence (:270-272) is what gets embedded."""
+        p = Path(pdf_path)
+        name = document_name or p.stem
+        if text is None:
+            text = extract_text(pdf_path) if extract_text is not None else extract_pdf_text(pdf_path)
+        if not text.strip():
+            text = (f"PDF Document: {p.stem}. Text extraction failed - may be image-based PDF "
+                    f"or corrupted.")
+        size = p.stat().st_size if p.exists() else 0
+        return self.process_text_document(text, name, str(pdf_path), size)
+
+    def process_all_data(self, data_directory, extract_text=None) -> None:
+        """embedding_generator.py:366-401: the directory's ';'-separated CSV tables, then
+        IngestedDocuments/*.json (parent document = the file name before " Table "), then
+        IngestedDocuments/*.pdf.  Files in name order (the reference: directory-listing order)."""
         d = Path(data_directory)
         for p in sorted(d.glob("*.csv")):
             self.process_csv_table(p)
-        for p in sorted(d.glob("*.json")):
-            self.process_json_table(p)
+        jd = d / "IngestedDocuments"
+        if jd.exists():
+            for p in sorted(jd.glob("*.json")):
+                parent = p.stem.split(" Table ")[0] if " Table " in p.stem else None
+                self.process_json_table(p, parent)
+            for p in sorted(jd.glob("*.pdf")):
+                self.process_pdf_document(p, p.stem, extract_text=extract_text)
 
     def embeddings_matrix(self) -> np.ndarray:
         if not self._chunks:
@@ -285,4 +385,5 @@ class BatchedEmbeddingGenerator:
 
 
 __all__ = ["EmbeddingStore", "BatchedEmbeddingGenerator", "analyze_data_patterns", "smart_text",
-           "flatten_json_to_text", "csv_record_documents", "read_csv_like_graph_builder"]
+           "flatten_json_to_text", "csv_record_documents", "read_csv_like_graph_builder",
+           "chunk_text", "extract_pdf_text"]

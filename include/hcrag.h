@@ -78,7 +78,9 @@ int hcr_index_add_device(hcr_index* index, const void* d_rows, int64_t n, int ro
                          int normalize, void* stream);
 
 /* Global id of this index's row 0 (row-sharded indexes: shard offset).  Search results
- * report id_offset + local row. */
+ * report id_offset + local row.  Fixed once hcr_index_add_ids has been used (HCR_EINVAL on a
+ * different value): rows then carry explicit ids, and plain adds after that get the ids
+ * id_offset + row at the time of the add. */
 int hcr_index_set_id_offset(hcr_index* index, int64_t id_offset);
 /* hcr_index_add with an explicit global id per row (host int64[n]); searches report these
  * ids for the appended rows (earlier rows keep id_offset + row).  Used by the multi-device
@@ -142,12 +144,20 @@ typedef struct {
   int32_t fallback_rounds;    /* K6/K7 rounds run (threshold tightenings + 1 per group) */
   int32_t score_kernel;       /* dense score kernel of the first pass: 1 register-staged
                                  128 x 128 (fp32 rows), 3 v3 (256 x 16 / 256 x 64), 4 v4
-                                 (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW */
+                                 (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW,
+                                 7 QW1 (one wave per SIMD, 64 / 48 queries per wave) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
  * is launched on; results appear in hcr_search_stats. */
 int hcr_index_set_timing(hcr_index* index, int enable);
+
+/* Tuning options of one index (results never change, only which exact kernel computes them).
+ *   HCR_OPT_QW1: large-batch kernel at D = 768 / 1024.  -1 = default heuristic, 0 = never QW1
+ *                (D = 768: QW, D = 1024: v4), 1 = QW1 with its DMA issue spread over the MFMA
+ *                groups, 2 = QW1 with the DMA issue at the stage barrier. */
+typedef enum { HCR_OPT_QW1 = 1 } hcr_index_option;
+int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)
  * into the global top-k (score desc, id asc).  Used after the cross-GPU exchange of
@@ -160,9 +170,9 @@ int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, i
  * Rows are sharded in contiguous blocks over `n_dev` devices (dev_ids may repeat: several
  * shards on one GPU); each hcr_multi_add splits its rows into n_dev blocks, ids stay insertion
  * order.  hcr_multi_search runs every shard's exact top-k concurrently (one host thread and
- * stream per shard), exchanges the per-shard lists to dev_ids[0] -- RCCL all-gather over the
- * distinct devices (ncclCommInitAll), or peer copies when devices repeat or RCCL is absent --
- * and merges them there (K5).  Same results as one hcr_index over all rows.  Replaces the
+ * stream per shard), gathers the per-shard lists on dev_ids[0] -- RCCL sends to it over the
+ * distinct devices (ncclCommInitAll), or peer copies when devices repeat, RCCL is absent or
+ * its communicators cannot be created -- and merges them there (K5).  Same results as one hcr_index over all rows.  Replaces the
  * single matrix of experiments/main.py:762 / the vector store behind
  * query_interface.py:200-204 when the corpus spans the GPUs of a node.
  * ------------------------------------------------------------------------------------- */
@@ -177,7 +187,7 @@ int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_t nq, int k
 int64_t hcr_multi_size(const hcr_multi_index* m);
 int hcr_multi_num_shards(const hcr_multi_index* m);
 int64_t hcr_multi_shard_size(const hcr_multi_index* m, int shard);
-/* 1: the last search exchanged lists by RCCL all-gather, 0: by peer copies. */
+/* 1: the last search gathered lists by RCCL point-to-point sends, 0: by peer copies. */
 int hcr_multi_exchange_kind(const hcr_multi_index* m);
 int hcr_multi_last_stats(const hcr_multi_index* m, hcr_search_stats* out);
 

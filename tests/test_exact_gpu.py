@@ -88,6 +88,29 @@ def test_large_k_exact_scan(hc):
             ix.search(Q, 2049)
 
 
+def test_large_k_sorted_corpus_converges(hc):
+    """a corpus ordered by ascending score against the query (the scan admits the
+    worst rows first).  K7's histogram threshold does not depend on admission order, so the
+    fallback converges in a few rounds instead of ~cap - k rows per round (1M rows, k = 2048:
+    the old rule needed ~160 rounds and failed at 64)."""
+    rng = np.random.default_rng(61)
+    N, D = 1_000_000, 64
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    q = rng.standard_normal(D).astype(np.float32)
+    E = E[np.argsort(E @ q, kind="stable")]            # ascending score: best rows last
+    Q = np.stack([q, -q, rng.standard_normal(D).astype(np.float32)])
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=False)
+        R = ix.get_rows()
+        for k in (2048, 300):
+            s, i = ix.search(Q, k)
+            st = ix.last_stats()
+            es, ei = O.cosine_topk(Q, R, k)
+            _check(s, i, es, ei)
+            assert st["fallback_queries"] == 3, st
+            assert st["fallback_rounds"] <= 8, st      # one group of 3 queries
+
+
 def test_threshold_is_fp64_and_inclusive(hc):
     """A row scoring exactly the threshold is kept (main.py:849 `>=`): the threshold crosses
     the ABI as a double and the scores come back in fp64 (a float threshold rounded
@@ -169,11 +192,13 @@ def test_add_ids_maps_results(hc):
             _check(s, i, es, ids[ei])
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0], "all"])
 def test_multi_device_index_matches_unsharded(hc, devices):
-    """hcr_multi_*: g shards (repeated device -> peer copies; one device -> the RCCL
-    all-gather path with one rank), several adds, mask, k beyond 256: same lists as the fp64
-    oracle over all rows."""
+    """hcr_multi_*: g shards (repeated device -> peer copies; distinct devices -> RCCL sends to
+    the first one; "all" = every visible GPU, one shard each), several adds, mask, k beyond
+    256: same lists as the fp64 oracle over all rows."""
+    if devices == "all":
+        devices = list(range(hc.device_count()))
     rng = np.random.default_rng(len(devices))
     N, D, B = 25000, 192, 40
     E = rng.standard_normal((N, D)).astype(np.float32)

@@ -1,18 +1,50 @@
 """Batched ingestion + on-disk store (experiments/embedding_generator.py).
 
 CPU: text construction worked by hand from embedding_generator.py:28-104 / :152-215 on small
-synthetic tables (parity with the reference's own outputs unpinned: the module needs
-sentence_transformers, absent here), metadata (:130-145), store round trip with no pickle,
-and one encode call per table.  GPU: the same through the MI355X encoder into a VectorIndex.
+synthetic tables; the product's texts and metadata over the reference's own data/ (CSV tables and
+IngestedDocuments JSON) against the independent restatement of tests/golden/make_ingest_f1.py
+(the reference module itself needs sentence_transformers, absent here); chunk_text (:278-305);
+store round trip with no pickle; one encode call per table / document.  GPU: the same data
+through the reference-precision MI355X encoder against the fixture's CPU BertModel fp32
+embeddings (<= 1e-4), then into a VectorIndex.
 """
+import gzip
 import json
+import os
+import shutil
 
 import numpy as np
 import pandas as pd
 import pytest
 
 from hcrag_amd.ingest import (BatchedEmbeddingGenerator, EmbeddingStore, analyze_data_patterns,
-                              flatten_json_to_text, smart_text)
+                              chunk_text, flatten_json_to_text, smart_text)
+
+F1 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f1")
+
+
+def _f1_data(tmp_path):
+    """The fixture's copy of the reference's data/ decompressed to tmp_path/data."""
+    src = os.path.join(F1, "data")
+    for dirpath, _, files in os.walk(src):
+        for f in files:
+            rel = os.path.relpath(os.path.join(dirpath, f), src)[:-3]       # strip .gz
+            dst = tmp_path / "data" / rel
+            dst.parent.mkdir(parents=True, exist_ok=True)
+            with gzip.open(os.path.join(dirpath, f), "rb") as fi, open(dst, "wb") as fo:
+                shutil.copyfileobj(fi, fo)
+    with gzip.open(os.path.join(F1, "expected.jsonl.gz"), "rt", encoding="utf-8") as fh:
+        expected = [json.loads(line) for line in fh]
+    return tmp_path / "data", expected
+
+
+def _relative_meta(metas, root):
+    out = []
+    for m in metas:
+        m = dict(m)
+        m["source_file"] = os.path.relpath(m["source_file"], root)
+        out.append(m)
+    return out
 
 
 class CountingEmbedder:
@@ -64,7 +96,9 @@ def test_json_flatten():
 
 def test_generator_batches_and_store_round_trip(tmp_path):
     df, p = _table(tmp_path)
-    (tmp_path / "doc.json").write_text(json.dumps({"title": "Spec", "parts": ["frame", "fork"]}))
+    (tmp_path / "IngestedDocuments").mkdir()
+    (tmp_path / "IngestedDocuments" / "doc.json").write_text(
+        json.dumps({"title": "Spec", "parts": ["frame", "fork"]}))
     emb = CountingEmbedder()
     g = BatchedEmbeddingGenerator(emb)
     g.process_all_data(tmp_path)
@@ -87,34 +121,97 @@ def test_generator_batches_and_store_round_trip(tmp_path):
     assert g2.get_statistics() == st
 
 
+def test_reference_data_texts_match_restatement(tmp_path):
+    """The reference's data/ (573 CSV rows of 7 tables + 6 IngestedDocuments JSON tables):
+    texts and metadata identical, in order, to the independent restatement's fixture; one
+    encode call per table / document."""
+    root, expected = _f1_data(tmp_path)
+    emb = CountingEmbedder()
+    g = BatchedEmbeddingGenerator(emb)
+    g.process_all_data(root)
+    assert g.embeddings_data["texts"] == [e["text"] for e in expected]
+    assert _relative_meta(g.embeddings_data["metadata"], tmp_path) == [e["metadata"] for e in expected]
+    assert len(emb.calls) == 7 + 6 and sum(emb.calls) == len(expected)
+    kinds = g.get_statistics()["content_types"]
+    assert kinds == {"database_table": 573, "json_table": 6}
+    parents = {e["metadata"]["parent_document"] for e in expected if e["metadata"]["type"] == "json_table"}
+    assert "Mountain Bike Manual" in parents
+
+
+def test_chunk_text_matches_restatement():
+    """chunk_text (:278-305) on the fixture's long document: identical chunks; the PDF item
+    texts / metadata of process_text_document (:307-364) identical too."""
+    with open(os.path.join(F1, "chunks.json"), encoding="utf-8") as fh:
+        fx = json.load(fh)
+    doc = fx["document"]
+    ch = chunk_text(doc, fx["chunk_size"], fx["overlap"])
+    prefix = f"PDF Document: {fx['document_name']}. "
+    assert [prefix + c for c in ch] == [it["text"] for it in fx["items"]]
+    emb = CountingEmbedder()
+    g = BatchedEmbeddingGenerator(emb)
+    n = g.process_text_document(doc, fx["document_name"], fx["items"][0]["metadata"]["source_file"], 0)
+    assert n == len(ch) and emb.calls == [n]                 # all chunks in one encode call
+    assert g.embeddings_data["metadata"] == [it["metadata"] for it in fx["items"]]
+    # edge cases of the reference loop
+    assert chunk_text("short.", 800, 100) == ["short."]
+    t = "a" * 1750                                           # no sentence end: hard cuts
+    assert [len(c) for c in chunk_text(t, 800, 100)] == [800, 800, 350]
+    t = ("x" * 30 + ". ") * 40                               # boundary search backs up to a '.'
+    assert all(c.endswith(".") for c in chunk_text(t, 800, 100)[:-1])
+
+
+def test_pdf_without_extractor_embeds_the_failure_text(tmp_path):
+    """No pdfplumber / PyPDF2 here: process_pdf_document embeds the reference's own
+    extraction-failure sentence (:270-272), as one chunk; an extractor callable is used when
+    given."""
+    pdf = tmp_path / "Manual.pdf"
+    pdf.write_bytes(b"%PDF-1.4 not really")
+    emb = CountingEmbedder()
+    g = BatchedEmbeddingGenerator(emb)
+    assert g.process_pdf_document(pdf) == 1
+    assert g.embeddings_data["texts"] == ["PDF Document: Manual. PDF Document: Manual. Text "
+                                          "extraction failed - may be image-based PDF or corrupted."]
+    assert g.embeddings_data["metadata"][0]["file_size"] == pdf.stat().st_size
+    assert g.process_pdf_document(pdf, "M2", extract_text=lambda p: "Page 1: hello. " * 80) == 2
+
+
 def test_store_rejects_mismatched_lengths(tmp_path):
     with pytest.raises(ValueError):
         EmbeddingStore.save(str(tmp_path / "s"), np.zeros((2, 4)), ["a"], [{}, {}])
 
 
 @pytest.mark.gpu
-def test_gpu_ingest_into_index(tmp_path):
-    """CSV rows -> one batched MI355X encode -> store -> VectorIndex: every row finds itself."""
+def test_gpu_ingest_reference_data_matches_cpu_bert(tmp_path):
+    """The reference's data/ through BatchedEmbeddingGenerator.process_all_data on the MI355X
+    encoder in reference precision (f32: split-f16 MFMA GEMMs, fp32 attention): every embedding
+    within 1e-4 of the fixture's CPU transformers BertModel fp32 (the configs[0] MiniLM-shape
+    seeded model), the long document's chunks too; then store -> VectorIndex, each row its own
+    nearest neighbour."""
     import hcrag_amd as hc
-    from hcrag_amd.encoder import BertEncoder, SentenceEmbedder, WordPieceTokenizer
-    from test_encoder_gpu import TINY, _hf_model
-    from hcrag_amd import config_from_hf
-    conf, m = _hf_model(TINY, 4)
-    chars = sorted(set("abcdefghijklmnopqrstuvwxyz0123456789-:,.;"))
-    vocab = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]", "table", "name", "product", "color"] + \
-        chars + ["##" + c for c in chars]
-    vocab = vocab[: TINY["vocab_size"]]
-    tok = WordPieceTokenizer(vocab_tokens=vocab)
-    enc = BertEncoder(config_from_hf(conf.to_dict(), "mean", True), m.state_dict(), dtype="f16")
-    emb = SentenceEmbedder(tok, enc, max_seq_length=64, batch_size=16)
-    df, p = _table(tmp_path)
+    from hcrag_amd.synthetic import bert_state
+    root, expected = _f1_data(tmp_path)
+    g0dir = os.path.join(os.path.dirname(F1), "configs0")
+    with open(os.path.join(g0dir, "goldens.json")) as fh:
+        g0 = json.load(fh)
+    cfg = dict(g0["model"])
+    state = bert_state(cfg, seed=g0["seed"], perturb_ln=g0["perturb_ln"])
+    tok = hc.WordPieceTokenizer(os.path.join(g0dir, "vocab.txt"), lowercase=True)
+    emb = hc.SentenceEmbedder(tok, hc.BertEncoder(cfg, state, dtype="f32"),
+                              max_seq_length=g0["max_seq_length"], batch_size=128)
+    ref = np.load(os.path.join(F1, "embeddings.npz"))
     g = BatchedEmbeddingGenerator(emb)
-    g.process_csv_table(p)
-    data = EmbeddingStore.load(g.save_embeddings(str(tmp_path / "store")))
-    E = np.asarray(data["embeddings"], np.float32)
-    ref = emb.encode(data["texts"])
-    np.testing.assert_allclose(E, ref, rtol=0, atol=2e-3)      # fp16 storage rounding
-    with hc.VectorIndex(E.shape[1], "f16") as ix:
-        ix.add(E, normalize=False)
-        _, ids = ix.search(ref.astype(np.float32), 1)
-        assert list(ids[:, 0]) == list(range(len(E)))
+    g.process_all_data(root)
+    assert g.embeddings_data["texts"] == [e["text"] for e in expected]
+    E = g.embeddings_matrix()
+    assert E.shape == ref["items"].shape
+    assert float(np.max(np.abs(E - ref["items"]))) <= 1e-4
+    with open(os.path.join(F1, "chunks.json"), encoding="utf-8") as fh:
+        fx = json.load(fh)
+    g2 = BatchedEmbeddingGenerator(emb)
+    g2.process_text_document(fx["document"], fx["document_name"])
+    assert float(np.max(np.abs(g2.embeddings_matrix() - ref["chunks"]))) <= 1e-4
+    data = EmbeddingStore.load(g.save_embeddings(str(tmp_path / "store"), dtype="f32"))
+    with hc.VectorIndex(E.shape[1], "f32") as ix:
+        ix.add(np.asarray(data["embeddings"], np.float32), normalize=False)
+        _, ids = ix.search(E[:64], 1)
+        assert list(ids[:, 0]) == list(range(64))
