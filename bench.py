@@ -65,6 +65,15 @@ def parse():
     p.add_argument("--sweep", default="1,8,32,64,256",
                    help="batch sizes of the 1-GPU small-batch sweep recorded in extra.batch_sweep "
                         "('' to skip)")
+    p.add_argument("--pipe-modes", default="f32,f16",
+                   help="encoder modes of the end-to-end query pipeline leg (token ids -> encoder "
+                        "-> sharded search), '' to skip")
+    p.add_argument("--pipe-steps", type=int, default=5)
+    p.add_argument("--no-configs1", action="store_true",
+                   help="skip the configs[1] leg (1M x 384 f16, B = 256, top-10; 1 GPU)")
+    p.add_argument("--no-configs4", action="store_true",
+                   help="skip the configs[4] per-rank leg (12.5M x 1024 bf16, 8192 queries, "
+                        "top-64, bge-large encoder; 1 GPU)")
     return p.parse_args()
 
 
@@ -238,6 +247,152 @@ def random_bert_state(cfg, seed=0):
             sd[p + nm + ".weight"] = np.ones(H, np.float32)
             sd[p + nm + ".bias"] = np.zeros(H, np.float32)
     return sd
+
+
+def enc_inputs(cfg, B, S, dev, seed):
+    """B ragged synthetic token sequences (lengths S/2..S, ids >= 1000, zero-padded) on dev."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    ids = torch.randint(1000, cfg["vocab_size"], (B, S), generator=g, dtype=torch.int32)
+    lens = torch.randint(S // 2, S + 1, (B,), generator=g)
+    mask = (torch.arange(S)[None, :] < lens[:, None]).to(torch.int32)
+    return (ids * mask).to(dev), mask.to(dev)
+
+
+def timed_steps(step, steps, dev, dist):
+    """Wall time of `steps` calls of step() bracketed by barrier + synchronize, max over ranks."""
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el / steps
+
+
+def pipeline_leg(a, hc, dev, rank, world, dist, searcher, B, nq, mode):
+    """The metric's end-to-end path (experiments/main.py:807-815 process_query: encode the query,
+    then find_similar_content; query_interface.py:200-204 'vector' mode): each rank's B query
+    token sequences -> the encoder (mode) -> ShardedSearch (all-gather of the embeddings, local
+    certified top-k on the shard, all-to-all, merge) on one stream.  Whole-job queries/s."""
+    cfg = ENC_SHAPES[a.encoder]
+    enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=mode, device=dev.index)
+    ids, mask = enc_inputs(cfg, B, a.enc_seq, dev, 177 + rank)
+    out = torch.empty((B, cfg["hidden"]), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        enc.encode_device(ids, mask, out, stream)
+        return searcher.search(out)
+    for _ in range(2):
+        step()
+    per = timed_steps(step, a.pipe_steps, dev, dist)
+    enc_only = timed_steps(lambda: enc.encode_device(ids, mask, out, stream), a.pipe_steps, dev, dist)
+    enc.close()
+    return {"mode": mode, "model": f"{a.encoder} shape, random init", "seq_len": a.enc_seq,
+            "queries_per_step": nq, "query_pipeline_qps": round(nq / per, 1),
+            "ms_per_step": round(per * 1e3, 3), "encoder_ms": round(enc_only * 1e3, 3),
+            "search_ms": round((per - enc_only) * 1e3, 3),
+            "path": "token ids -> encoder -> all-gather -> certified top-k -> all-to-all -> merge"
+                    if world > 1 else "token ids -> encoder -> certified top-k (one stream)"}
+
+
+def configs1_leg(a, hc, dev, steps=50):
+    """BASELINE.json configs[1] on one GPU: 1M x 384 f16 (L2-normalised N(0,1) rows), 256
+    queries (half planted), top-10.  HBM-bound (256 flop/B < the 312 ridge): the roofline is the
+    corpus stream, 0.768 GB per batch = 96 us at 8 TB/s."""
+    N, D, B, k = 1_000_000, 384, 256, 10
+    ix = hc.VectorIndex(D, "f16", device=dev.index, capacity=N)
+    make_shard(ix, hc, 0, N, D, "f16", dev, seed=2000)
+
+    def rows_fn(idx):
+        return torch.stack([torch.from_numpy(ix.get_rows(i, 1)[0]) for i in idx.tolist()]).to(dev)
+    Q, src = make_queries(rows_fn, B, D, dev, 0, N, 0)
+    S = torch.empty((B, k), dtype=torch.float64, device=dev)
+    I = torch.empty((B, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
+    for _ in range(5):
+        step()
+    per = timed_steps(step, steps, dev, None)
+    ix.set_timing(True)
+    km = 0.0
+    for _ in range(steps):
+        step()
+        km += ix.last_stats()["score_kernel_ms"]
+    ix.set_timing(False)
+    st = ix.last_stats()
+    km /= steps
+    recall = float((I[: B // 2, 0].cpu() == src.cpu()).float().mean().item())
+    byt = N * D * 2 + B * D * 2 + B * k * 12
+    ix.close()
+    return {"workload": "configs[1]: 1,000,000 x 384 f16 node embeddings, batch=256 queries, "
+                        "top-10, 1 GPU", "qps": round(B / per, 1), "ms_per_step": round(per * 1e3, 4),
+            "score_kernel_ms": round(km, 4), "hbm_frac_step": round(byt / per / 1e9 / HBM_PEAK_GBS, 4),
+            "hbm_frac_kernel": round(byt / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "alg_bytes": byt, "score_kernel": st.get("score_kernel"), "kprime": st["kprime"],
+            "planted_recall_at_1": recall, "uncertified_queries": st["uncertified_queries"],
+            "note": "ms_per_step = wall time of one hcr_search_device call (queries in HBM, its one "
+                    "host sync included); score_kernel_ms = HIP events around the pre-pass + dense "
+                    "score launches"}
+
+
+def configs4_leg(a, hc, dev, steps=3):
+    """BASELINE.json configs[4] at its per-rank shape on one GPU: a 12.5M x 1024 bf16 shard
+    (100M / 8), the global batch of 8192 queries, top-64, with this rank's 1024 queries encoded
+    by the bge-large-shape encoder (reference precision) in the same step; the other ranks'
+    7168 embeddings stand in for the all-gather (exchange time excluded: one GPU)."""
+    N, D, B, k, own = 12_500_000, 1024, 8192, 64, 1024
+    cfg = ENC_SHAPES["bge-large"]
+    ix = hc.VectorIndex(D, "bf16", device=dev.index, capacity=N)
+    make_shard(ix, hc, 0, N, D, "bf16", dev, seed=3000)
+    enc = hc.BertEncoder(cfg, random_bert_state(cfg, seed=1), dtype="f32", device=dev.index)
+    ids, mask = enc_inputs(cfg, own, a.enc_seq, dev, 401)
+    g = torch.Generator(device=dev).manual_seed(402)
+    Q = torch.randn((B, D), generator=g, device=dev)
+    Qown = Q[:own]                                         # rows 0..1023: this rank's queries
+    S = torch.empty((B, k), dtype=torch.float64, device=dev)
+    I = torch.empty((B, k), dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def search():
+        ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
+
+    def step():
+        enc.encode_device(ids, mask, Qown, stream)
+        search()
+    step()
+    per = timed_steps(step, steps, dev, None)
+    ix.set_timing(True)
+    km = 0.0
+    for _ in range(steps):
+        search()
+        km += ix.last_stats()["score_kernel_ms"]
+    ix.set_timing(False)
+    st = ix.last_stats()
+    km /= steps
+    srch = timed_steps(search, steps, dev, None)
+    enc.close()
+    ix.close()
+    fl = 2.0 * B * N * D
+    return {"workload": "configs[4] per-rank shape: 12,500,000 x 1024 bf16 shard, 8192 queries "
+                        "(1024 encoded here by bge-large f32), top-64, 1 GPU",
+            "per_rank_ms": round(per * 1e3, 3), "search_ms": round(srch * 1e3, 3),
+            "encoder_ms": round((per - srch) * 1e3, 3), "score_kernel_ms": round(km, 3),
+            "mfma_frac_score": round(fl / (km * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
+            "mfma_frac_search": round(fl / srch / 1e12 / MFMA_PEAK_TFLOPS, 4),
+            "est_8gpu_qps": round(B / per, 1), "score_kernel": st.get("score_kernel"),
+            "kprime": st["kprime"], "workgroups": st["workgroups"],
+            "uncertified_queries": st["uncertified_queries"],
+            "note": "est_8gpu_qps = 8192 / per-rank step (each of 8 ranks holds 12.5M rows and "
+                    "scores all 8192 queries); the all-gather / all-to-all are not in it"}
 
 
 def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
@@ -529,9 +684,20 @@ def main():
         for mode in [m for m in a.enc_modes.split(",") if m]:
             enc_res[mode] = encoder_leg(a, hc, dev, rank, world, dist, mode, B)
 
+    pipe = None
+    if a.pipe_modes and a.encoder != "none" and ENC_SHAPES[a.encoder]["hidden"] == D:
+        pipe = {}
+        for mode in [m for m in a.pipe_modes.split(",") if m]:
+            pipe[mode] = pipeline_leg(a, hc, dev, rank, world, dist, searcher, B, nq, mode)
+            log(json.dumps({"pipeline": pipe[mode]}))
+
     sweep = None
     if a.sweep and world == 1 and rank == 0:
         sweep = batch_sweep(a, ix, dev, nloc, D, k)
+    c1 = c4 = None
+    if rank == 0 and world == 1 and not a.no_configs1:
+        c1 = configs1_leg(a, hc, dev)
+        log(json.dumps({"configs1": c1}))
     c0 = None
     if rank == 0 and world == 1 and not a.no_configs0:
         c0 = configs0_leg(hc)
@@ -551,6 +717,9 @@ def main():
             "cpu_baseline": cpu,
             "encoder": enc_res,
             "configs0": c0,
+            "configs1": c1,
+            "query_pipeline": pipe,
+            "query_pipeline_qps": (pipe or {}).get("f32", {}).get("query_pipeline_qps"),
             "extra": {"planted_recall_at_1": recall1, "uncertified_queries": unc,
                       "widened_queries": widened, "fallback_queries": fallback,
                       "kprime": st["kprime"], "unit_kernel": st["unit_kernel"],
@@ -561,8 +730,14 @@ def main():
                       "pipeline_ms_per_step": round(elapsed / a.steps * 1e3, 3),
                       "batch_sweep": sweep},
         }
-        print(json.dumps(line), flush=True)
     ix.close()
+    if rank == 0 and world == 1 and not a.no_configs4:
+        torch.cuda.empty_cache()
+        c4 = configs4_leg(a, hc, dev)
+        log(json.dumps({"configs4_rank": c4}))
+    if rank == 0:
+        line["configs4_rank"] = c4
+        print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 

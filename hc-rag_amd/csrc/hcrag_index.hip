@@ -63,6 +63,7 @@ struct hcr_index {
       f_hcnt, f_hmin;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
+  int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -409,8 +410,12 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   switch (option) {
     case HCR_OPT_QW1:
-      if (value < -1 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 2]", value);
+      if (value < -1 || value > 5) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 5]", value);
       ix->opt_qw1 = value;
+      return HCR_OK;
+    case HCR_OPT_QW1_SHAPE:
+      if (value < 0 || value > 3) return set_err(HCR_EINVAL, "HCR_OPT_QW1_SHAPE value %d not in [0, 3]", value);
+      ix->opt_qw1_shape = value;
       return HCR_OK;
     default:
       return set_err(HCR_EINVAL, "unknown index option %d", option);
@@ -478,7 +483,7 @@ struct TestHooks {
   int qs_max = 256;
   int qw_min = 0;                    // 0: the measured default (v3_cfg)
   int qw1 = -1;                      // HCR_OPT_QW1 default (-1: the heuristic)
-  bool no_prepass = false, rigorous_seed = false, prepass_topk = false;
+  bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -487,8 +492,9 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
     if (const char* e = getenv("HCRAG_QS_MAX")) t.qs_max = atoi(e);
     if (const char* e = getenv("HCRAG_QW_MIN")) t.qw_min = std::max(1, atoi(e));
-    if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(2, std::max(-1, atoi(e)));
+    if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(5, std::max(-1, atoi(e)));
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
+    t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -501,10 +507,11 @@ static const TestHooks& hooks() {
 
 // qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h); qw1: the
 // one-wave-per-SIMD form (score_qw1.h), spread = its DMA issue spread over the MFMA groups
-struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false; };
+struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false, nw8 = false, pipe = false; };
 // qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
 // QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1
-static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1) {
+static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1,
+                    int qw1_shape = 0) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
@@ -517,8 +524,11 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   // from 257 queries by default; D = 768 only when asked (HCR_OPT_QW1).
   if (opt_qw1 != 0 && unit_ok && qw1_ok && qw1_supported(ld)) {
     const bool d1024 = ld / V3_BK == 32;
-    if ((opt_qw1 > 0 || d1024) && nq >= (d1024 ? 257 : qw_from))
-      return {qw1_rows(ld), qw1_queries(ld), 0, false, false, true, opt_qw1 != 2};
+    const bool nw8 = (opt_qw1 == 3 || opt_qw1 == 4) && qw1_nw8_supported(ld);   // 8-wave form (D = 384)
+    const bool pipe = opt_qw1 == 5;                                 // QW1P (score_qw1p.h)
+    if ((opt_qw1 > 0 || d1024) && nq >= (d1024 ? 257 : ld / V3_BK == 12 ? 129 : qw_from))
+      return {qw1_rows(ld, pipe ? kQw1Pipelined : qw1_shape), qw1_queries(ld), 0, false, false, true,
+              opt_qw1 != 2 && opt_qw1 != 4, nw8, pipe};
   }
   if (nq >= qw_from && unit_ok && qw_ok && qw_supported(ld))
     return {qw_rows(ld), kQwQueries, kQwStages, false, true};
@@ -565,7 +575,9 @@ __global__ void unit_dev_kernel(const float* __restrict__ inv32, int64_t n,
   m = wave_max_f64(m);
   if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(out, (unsigned long long)__double_as_longlong(m));
 }
-static constexpr double kUnitDevMax = 1.0 / 1024;   // UNIT kernels for L2-normalised corpora
+// UNIT kernels for L2-normalised corpora when max_r |1/inv32_r - 1| <= 2^-9 (f16 rows: ~5e-5;
+// bf16 rows after the ingest's scale search: < 1e-3)
+static constexpr double kUnitDevMax = 1.0 / 512;
 
 template <typename TM, int CAP, int RT, int QT, int WM, int WN, int NST>
 static void launch_v3_t(hcr_index* ix, V3Launch a, hipStream_t st) {
@@ -587,11 +599,13 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
   return launch_qs(ix->dtype, q, st);
 }
 
-static int launch_qw1_ix(hcr_index* ix, V3Launch a, int cap, bool spread, hipStream_t st) {
+static int launch_qw1_ix(hcr_index* ix, V3Launch a, int cap, bool spread, bool nw8, bool pipe,
+                         hipStream_t st) {
   QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
            a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
-  return launch_qw1(ix->dtype, q, spread, st);
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true,
+           pipe ? kQw1Pipelined : ix->opt_qw1_shape};
+  return launch_qw1(ix->dtype, q, spread, nw8, st);
 }
 
 // Row partitions of a QW1 launch (one workgroup per CU, LDS-bound): the smallest P >= 256 / nqb
@@ -669,7 +683,7 @@ template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
   if (c.qs) return launch_qs_ix(ix, c, a, st);              // CAP chosen in score_qs.hip
   if (c.qw) return launch_qw_ix(ix, a, cap, st);
-  if (c.qw1) return launch_qw1_ix(ix, a, cap, c.spread, st);
+  if (c.qw1) return launch_qw1_ix(ix, a, cap, c.spread, c.nw8, c.pipe, st);
   switch (cap) {
     case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
     case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
@@ -817,8 +831,14 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
                           qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
-                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1);
+                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qw1_shape);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
+  if (hooks().debug_cfg)
+    fprintf(stderr, "[hcrag] search_pass nq=%d n=%lld ld=%d kp=%d unit_dev=%.3g rho=%.3g mask=%d "
+                    "qw1_opt=%d -> ver=%d rt=%d qt=%d qs=%d qw=%d qw1=%d\n", nq, (long long)ix->n,
+            ix->ld, kp, ix->unit_dev_host, ix->rho_host, (int)ix->has_mask,
+            ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ver, c3.rt, c3.qt, (int)c3.qs,
+            (int)c3.qw, (int)c3.qw1);
   const int tq = ver == 3 ? c3.qt : BQ, tr = ver == 3 ? c3.rt : BR;
   const bool qs = ver == 3 && c3.qs, qw = ver == 3 && c3.qw, qw1 = ver == 3 && c3.qw1;
   // QS batches are padded to 256 queries for their MAXONLY pre-pass on the 256 x 256 kernel
@@ -833,6 +853,8 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                : qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
+  // final lists per (query, partition): the 8-wave QW1 writes one per row half
+  const int PL = P * (qw1 && c3.nw8 ? 2 : 1);
   const bool tm_f16 = ix->dtype == HCR_F16;
   const size_t tms = 2;
 
@@ -840,11 +862,11 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_qnorm.ensure((size_t)nqpad * 8));
   CHECK(ix->w_eps.ensure((size_t)nqpad * 8));
   CHECK(ix->w_taug.ensure((size_t)nqpad * 4));
-  CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8));
-  CHECK(ix->w_part.ensure((size_t)nqpad * P * kp * 8));
-  CHECK(ix->w_pcnt.ensure((size_t)nqpad * P * 4));
-  CHECK(ix->w_merged.ensure(merge_workspace_keys(nqpad, P, kp) * 8));
-  CHECK(ix->w_mcnt.ensure((size_t)nqpad * ((P + merge_groups(kp) - 1) / merge_groups(kp)) * 4 * 2));
+  CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8 * (PL / P)));
+  CHECK(ix->w_part.ensure((size_t)nqpad * PL * kp * 8));
+  CHECK(ix->w_pcnt.ensure((size_t)nqpad * PL * 4));
+  CHECK(ix->w_merged.ensure(merge_workspace_keys(nqpad, PL, kp) * 8));
+  CHECK(ix->w_mcnt.ensure((size_t)nqpad * ((PL + merge_groups(kp) - 1) / merge_groups(kp)) * 4 * 2));
   CHECK(ix->w_unc.ensure((size_t)nqpad * 4));
   CHECK(ix->w_cnt.ensure(16));
   CHECK(ix->w_tauest.ensure((size_t)nqpad * 4));
@@ -866,7 +888,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
   if (ix->stats.score_kernel == 0)
-    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? 7 : qw ? 6 : qs ? 5 : wide ? 4 : 3;
+    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? (c3.pipe ? 9 : c3.nw8 ? 8 : 7) : qw ? 6 : qs ? 5 : wide ? 4 : 3;
 
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)
@@ -948,7 +970,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
-  CHECK(merge_lists(ix, nq, nqpad, P, kp, st, &merged_ptr));
+  CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr));
 
   if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
   else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);

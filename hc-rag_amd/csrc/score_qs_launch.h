@@ -18,7 +18,8 @@ struct QsArgs {
   int kp;
   int cap;                   // qs_cap(kp)
   bool unit;                 // raw dot products as coarse scores (L2-normalised corpus)
-  int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles)
+  int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles);
+                             // QW1: its tuning shape (HCR_OPT_QW1_SHAPE)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128
@@ -43,7 +44,10 @@ constexpr int kQwStages = 3;          // QW ring stages (= QW_NST)
 // One-wave-per-SIMD query-stationary kernel (score_qw1.h): 256 (D = 768) or 192 (D = 1024)
 // queries per workgroup, UNIT corpora without a row mask.
 bool qw1_supported(int ld);
-int qw1_rows(int ld);                 // rows per stage (the kernel's row tile)
+int qw1_rows(int ld, int shape);      // rows per stage (the kernel's row tile) of a tuning shape
 int qw1_queries(int ld);              // queries per workgroup
 int qw1_cap(int kp, int ld);          // candidate buffer slots per query (0: k' too large)
-int launch_qw1(int dtype, const QsArgs& a, bool spread, hipStream_t st);
+bool qw1_nw8_supported(int ld);       // the 8-wave form (two row halves per query set): D = 384
+constexpr int kQw1Pipelined = 4;      // QsArgs::nq_blocks / qw1_rows shape of QW1P (score_qw1p.h)
+// nw8: the 8-wave form, whose final lists are P x 2 per query (row half h of partition p: 2p + h)
+int launch_qw1(int dtype, const QsArgs& a, bool spread, bool nw8, hipStream_t st);

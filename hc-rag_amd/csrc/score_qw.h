@@ -71,6 +71,23 @@ __device__ __forceinline__ void qw_frag_wait(V (&av)[2]) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(av[0]), "+v"(av[1]) : "n"(N) : "memory");
 }
 
+// Epilogue helpers of the query-stationary kernels (the per-stage test "does any of a query's
+// scores reach its threshold"), without fmaxf's sNaN canonicalisation (a v_max per operand) and
+// the float <-> ordered-key round trips: v_max3_f32 over the raw accumulators (a quiet NaN, the
+// mark of rows past the corpus, never wins a maximum unless every operand is one), and the
+// threshold kept as an ordered key: max(high word of the local k'-th key, the global bound).
+// The caller has covered the MFMA -> VALU wait states of the accumulators (asm operands).
+__device__ __forceinline__ float qw_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float qw_max4(const floatx4& v) { return qw_max3(qw_max3(v[0], v[1], v[2]), v[3], v[3]); }
+__device__ __forceinline__ uint32_t qw_ord32(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+}
+
 template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,

@@ -35,6 +35,19 @@ namespace hcr {
 
 constexpr int QW1_NW = 4;       // waves per workgroup: one per SIMD
 
+#ifdef HCR_QW1_STAMPS
+// Diagnostic build only (Makefile target `stamps_qw1`, tools/qw1_stamps.py): per wave, s_memtime
+// cycles summed over the stages: [0] vmcnt wait + barrier, [1] DMA issue + bounds / first
+// fragment reads, [2] the MFMA groups, [3] the epilogue, [4] stages.  Never in the product.
+__device__ unsigned long long hcr_qw1_stamps[4096 * 8 * 8];
+#define HCR_QW1_STAMP(t)                                                               \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#endif
+
 // f(std::integral_constant<int, I>{}) for I = 0 .. N-1: compile-time indices (asm immediates)
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -46,22 +59,37 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int KS> struct Qw1Shape;
 template <> struct Qw1Shape<24> { static constexpr int QB = 4, SR = 32, NST = 3; };   // D = 768
 template <> struct Qw1Shape<32> { static constexpr int QB = 3, SR = 16, NST = 4; };   // D = 1024
+// D = 384 (configs[1]: HBM-bound at 256 queries): 24 KiB stages, 5 in flight
+template <> struct Qw1Shape<12> { static constexpr int QB = 4, SR = 32, NST = 6; };
 
-template <int KS, int QB = Qw1Shape<KS>::QB, int SR_ = Qw1Shape<KS>::SR, int NST_ = Qw1Shape<KS>::NST>
+// NW = 8 ("QW2", D = 384 only: 64 queries x 384 k = 192 registers, so two waves fit a SIMD):
+// waves w and w + 4 hold the same 64 queries and take the two row halves of every stage, each
+// with its own candidate buffers and final lists (row half h of partition p is list 2 p + h), so
+// the partner wave on the SIMD hides DMA issue, epilogues and barrier skew while each row
+// fragment is still read by only 4 waves.
+template <int KS, int NW = QW1_NW> struct Qw1Shape2 : Qw1Shape<KS> {};
+template <> struct Qw1Shape2<12, 8> { static constexpr int QB = 4, SR = 32, NST = 5; };
+
+template <int KS, int NW = QW1_NW, int QB = Qw1Shape2<KS, NW>::QB, int SR_ = Qw1Shape2<KS, NW>::SR,
+          int NST_ = Qw1Shape2<KS, NW>::NST>
 struct Qw1Layout {
   static constexpr int SR = SR_, RB = SR / 16, NST = NST_;
+  static constexpr int H = NW / QW1_NW;                     // row halves (waves per query set)
+  static constexpr int RBW = RB / H;                        // row blocks per wave per stage
   static constexpr int QPW = 16 * QB, QT = QW1_NW * QPW;  // queries per wave / workgroup
   static constexpr int PIECES = RB * KS;                    // 1 KiB pieces per stage
-  static constexpr int PPW = PIECES / QW1_NW;               // ... per wave
+  static constexpr int PPW = PIECES / NW;                   // ... per wave
   static constexpr int STAGE = PIECES * 1024;
-  static constexpr int TGS = NST * STAGE;                   // [NST][4 waves][64 lanes] u32 bounds
-  static constexpr int TAU = TGS + NST * QW1_NW * 256;      // u64 tau_key[QT]
-  static constexpr int CNT = TAU + QT * 8;                  // int cnt[QT]
-  static constexpr int TOTAL = CNT + QT * 4;
+  static constexpr int TGS = NST * STAGE;                   // [NST][NW waves][64 lanes] u32 bounds
+  static constexpr int TAU = TGS + NST * NW * 256;          // u64 tau_key[H][QT]
+  static constexpr int CNT = TAU + H * QT * 8;              // int cnt[H][QT]
+  static constexpr int TOTAL = CNT + H * QT * 4;
   static constexpr int NF = QB * KS;                        // query fragments per wave
-  static constexpr int FA = NF < 64 ? NF : 64;              // ... of them in AGPRs
+  // ... of them in AGPRs: 64 (256 registers) at one wave per SIMD; with two waves each wave's
+  // 256 registers split evenly (accum_offset 128), so 32
+  static constexpr int FA = NF < 64 / H ? NF : 64 / H;
   static constexpr int FV = NF - FA;                        // ... in VGPRs
-  static_assert(SR > 0 && (RB == 1 || RB % 2 == 0) && PIECES % QW1_NW == 0, "QW1 stage shape");
+  static_assert(SR > 0 && RBW >= 1 && (RBW == 1 || RBW % 2 == 0) && PIECES % NW == 0, "QW1 stage shape");
   static_assert(QPW <= 64, "one 4-byte bound per lane");
   static_assert(STAGE <= 65536, "group offsets in the 16-bit ds_read offset field");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -103,22 +131,27 @@ __device__ __forceinline__ void qw1_issue_frags(uint32_t vbase, V (&av)[2]) {
                : "memory");
 }
 
-template <typename TM, int CAP, int KS, bool SPREAD>
-__global__ void __launch_bounds__(QW1_NW * 64, 1)
+// SR_ / NST_ / FD_: overrides of the shape's stage rows, ring depth and fragment groups in flight
+// (0 = the shape's; tuning variants, HCR_OPT_QW1_SHAPE)
+template <typename TM, int CAP, int KS, bool SPREAD, int NW = QW1_NW, int SR_ = 0, int NST_ = 0,
+          int FD_ = 0>
+__global__ void __launch_bounds__(NW * 64, NW / QW1_NW)
 score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                       const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                       uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                       uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = Qw1Layout<KS>;
+  using L = Qw1Layout<KS, NW, Qw1Shape2<KS, NW>::QB, SR_ ? SR_ : Qw1Shape2<KS, NW>::SR,
+                      NST_ ? NST_ : Qw1Shape2<KS, NW>::NST>;
   using V = typename MfmaOp<TM>::V;
   using M = Qw1Mfma<TM>;
-  constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = L::QT, QPW = L::QPW, NST = L::NST;
-  constexpr int QB = QPW / 16, D = NST - 1, FA = L::FA, FV = L::FV;
+  constexpr int SR = L::SR, RB = L::RBW, PPW = L::PPW, QT = L::QT, QPW = L::QPW, NST = L::NST;
+  constexpr int QB = QPW / 16, D = NST - 1, FA = L::FA, FV = L::FV, H = L::H;
   constexpr int OPS = PPW + 1;                        // vmcnt-counted ops per wave per stage
-  // fragment groups per stage: (row-block pair, k-step), or (row block, k-step pair) if RB = 1
+  // fragment groups per stage (of the wave's RB row blocks): (row-block pair, k-step), or
+  // (row block, k-step pair) if RB = 1
   constexpr int NG = RB == 1 ? KS / 2 : (RB / 2) * KS;
   constexpr int OFF2 = (RB == 1 ? 1 : KS) * 1024;
-  constexpr int FD = 3;                               // fragment groups in flight
+  constexpr int FD = FD_ ? FD_ : H == 1 ? 3 : 2;      // fragment groups in flight (NW = 8: VGPRs)
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -126,6 +159,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qset = wave & (QW1_NW - 1), half = wave / QW1_NW;   // query set, row half
 
   const int nwg = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -134,12 +168,15 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int t0 = (int)((int64_t)p * ntiles / P);
   const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
   const int qbase = qb * QT;
-  uint64_t* wbuf = buf + (size_t)b * QT * CAP;
-  const int wq0 = wave * QPW;                         // this wave's first query (block-local)
+  uint64_t* wbuf = buf + ((size_t)b * H + half) * QT * CAP;
+  const int wq0 = qset * QPW;                         // this wave's first query (block-local)
+  tau_key += half * QT;                               // this row half's per-query state
+  cnt += half * QT;
+  const int PH = P * H, ph = p * H + half;            // this wave's final list: (query, ph)
 
   if (lane < QPW) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
   if (t0 >= t1) {
-    if (lane < QPW) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
+    if (lane < QPW) pcnt[(size_t)(qbase + wq0 + lane) * PH + ph] = 0;
     return;
   }
 
@@ -170,7 +207,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   const int nsteps = t1 - t0;
   // Stage i (tile t0 + i) goes to ring slot i % NST: this wave's PPW row pieces (piece j =
-  // wave + 4 u: row block j / KS, k-step j % KS) and its global bounds -- OPS ops.  Stages past
+  // wave + NW u: row block j / KS, k-step j % KS) and its global bounds -- OPS ops.  Stages past
   // the partition's end are issued through zero-record descriptors (nothing is read; their LDS
   // writes land in a slot already consumed), so the loop has no tail cases.
   struct StageDesc { __amdgpu_buffer_rsrc_t a, t; int slot; };
@@ -187,14 +224,14 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   };
   auto issue_op = [&](const StageDesc& d, int u) __attribute__((always_inline)) {
     if (u < PPW) {
-      const int j = wave + QW1_NW * u;
+      const int j = wave + NW * u;
       dma16(d.a, lds + d.slot * L::STAGE + j * 1024, voff, (j / KS) * 16 * ldb + (j % KS) * (V3_BK * 2));
     } else {
       int tv;   // the lane's byte offset, opaque (a hoisted copy would be spilled)
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
                    "v_lshlrev_b32 %0, 2, %0" : "=v"(tv));
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * QW1_NW + wave) * 256),
+          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * NW + wave) * 256),
           4, tv, wq0 * 4, 0, 0);
     }
   };
@@ -211,9 +248,18 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   uint64_t tkr[QB];
 #pragma unroll
   for (int n = 0; n < QB; ++n) tkr[n] = 0ull;
+#ifdef HCR_QW1_STAMPS
+  uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
+#endif
   for (int s = 0; s < nsteps; ++s) {
+#ifdef HCR_QW1_STAMPS
+    HCR_QW1_STAMP(st_t0);
+#endif
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
+#ifdef HCR_QW1_STAMPS
+    HCR_QW1_STAMP(st_t1);
+#endif
     const StageDesc nd = stage_desc(s + D);
     if constexpr (!SPREAD) {
 #pragma unroll
@@ -222,15 +268,17 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
     const int slot = s % NST;
     const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
+    // the wave's row half: its first row block's pieces (a wave-uniform offset of the stage)
+    const uint32_t sth = (uint32_t)__builtin_amdgcn_readfirstlane((int)(st + (uint32_t)(half * RB * KS * 1024)));
     uint32_t vbase;
-    asm volatile("v_add_u32 %0, %1, %2" : "=v"(vbase) : "s"(st), "v"(offA));
+    asm volatile("v_add_u32 %0, %1, %2" : "=v"(vbase) : "s"(sth), "v"(offA));
     // this stage's global bounds of the lane's QB queries: read now, waited for with the last
     // fragment group
     uint32_t tg[QB];
     {
       int le0;
       asm volatile("v_mov_b32 %0, %1" : "=v"(le0) : "v"(lane));
-      const uint32_t ta = lds_addr(lds + L::TGS + (slot * QW1_NW + wave) * 256 + (le0 & 15) * 4);
+      const uint32_t ta = lds_addr(lds + L::TGS + (slot * NW + wave) * 256 + (le0 & 15) * 4);
       static_for<QB>([&](auto nc) {
         constexpr int N = decltype(nc)::value;
         uint32_t& t = tg[N];       // (named outside the asm: operands alone do not capture)
@@ -238,6 +286,9 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         asm volatile("ds_read_b32 %0, %1 offset:%2" : "=&v"(t) : "v"(a), "n"(N * 64) : "memory");
       });
     }
+#ifdef HCR_QW1_STAMPS
+    HCR_QW1_STAMP(st_t2);
+#endif
     floatx4 acc[RB][QB];
     V av[FD][2];
     // group J: row blocks (2 (J / KS), +1) at k-step J % KS (RB >= 2), or row block 0 at
@@ -296,6 +347,9 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         });
       }
     });
+#ifdef HCR_QW1_STAMPS
+    HCR_QW1_STAMP(st_t3);
+#endif
     // MFMA results -> VALU readers: the XDL write-back wait states the compiler does not see
     // (the MFMAs are asm), with every accumulator named so nothing reads one earlier
 #pragma unroll
@@ -313,8 +367,8 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
     const int lq = le >> 4;
     const int qle = wq0 + (le & 15);                 // the query of accumulator block 0
-    const int64_t row0 = (int64_t)(t0 + s) * SR;
-    if (row0 + SR > n_rows) {      // the corpus' last tile: rows past the end never pass (NaN)
+    const int64_t row0 = (int64_t)(t0 + s) * SR + half * RB * 16;   // the wave's first row
+    if (row0 + RB * 16 > n_rows) { // the corpus' last tile: rows past the end never pass (NaN)
 #pragma unroll
       for (int m = 0; m < RB; ++m)
 #pragma unroll
@@ -323,20 +377,21 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
             for (int n = 0; n < QB; ++n) acc[m][n][r] = __builtin_nanf("");
     }
-    float thr[QB];
     bool hit[QB];
     bool any_hit = false;
 #pragma unroll
     for (int n = 0; n < QB; ++n) {
-      thr[n] = fmaxf(tkr[n] ? key_score(tkr[n]) : -INFINITY, unord32(tg[n]));
-      float mx = -INFINITY;
+      float mx = qw_max4(acc[0][n]);
 #pragma unroll
-      for (int m = 0; m < RB; ++m)
-        mx = fmaxf(mx, fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])));
-      hit[n] = mx >= thr[n];
+      for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
+      const uint32_t tk = max((uint32_t)(tkr[n] >> 32), tg[n]);
+      hit[n] = qw_ord32(mx) >= tk;       // (a NaN maximum passes here; its scores fail below)
       any_hit |= hit[n];
     }
     if (__any(any_hit)) {
+      float thr[QB];
+#pragma unroll
+      for (int n = 0; n < QB; ++n) thr[n] = unord32(max((uint32_t)(tkr[n] >> 32), tg[n]));
       const uint32_t row0u = (uint32_t)row0;
 #pragma unroll
       for (int n = 0; n < QB; ++n) {
@@ -377,11 +432,24 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         for (int n = 0; n < QB; ++n) tkr[n] = v3_lds_u64(tau_key + qle + 16 * n);
       }
     }
+#ifdef HCR_QW1_STAMPS
+    HCR_QW1_STAMP(st_t4);
+    st_acc[0] += st_t1 - st_t0;
+    st_acc[1] += st_t2 - st_t1;
+    st_acc[2] += st_t3 - st_t2;
+    st_acc[3] += st_t4 - st_t3;
+#endif
   }
+#ifdef HCR_QW1_STAMPS
+  if (lane == 0 && b < 4096) {
+    unsigned long long* o = hcr_qw1_stamps + ((size_t)b * 8 + wave) * 8;
+    o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = st_acc[3]; o[4] = nsteps;
+  }
+#endif
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + QPW, kp, lane, partials, pcnt, P, p);
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + QPW, kp, lane, partials, pcnt, PH, ph);
 }
 
 }  // namespace hcr

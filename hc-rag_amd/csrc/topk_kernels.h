@@ -46,6 +46,29 @@ ingest_kernel(const TIN* __restrict__ in, int64_t n, int dim, int ld, int normal
     ss = wave_sum_f64(ss);
     const double nr = sqrt(ss);
     scale = (nr < 10.0 * 2.220446049250313e-16) ? 1.0 : 1.0 / nr;
+    // 16-bit storage: the ROUNDED row's norm misses 1 by the rounding (bf16: up to ~2e-3 over
+    // 10M rows), which widens the UNIT kernels' certificate.  Of the 17 scales
+    // scale * (1 + t 2^-12), |t| <= 8, keep the one whose rounded row's norm is closest to 1
+    // (bf16: max deviation ~2e-3 -> ~6e-4): every stored row is still the input direction,
+    // rounded once.
+    if constexpr (sizeof(TS) == 2) {
+      if (scale != 1.0 || nr == 1.0) {
+        double best = 1e30, best_scale = scale;
+        for (int t = 0; t <= 16; ++t) {
+          const double sc = scale * (1.0 + (double)((t + 1) / 2 * ((t & 1) ? 1 : -1)) * 2.44140625e-4);
+          double s2 = 0.0;
+          for (int d = lane; d < dim; d += 64) {
+            const double xd = (double)(float)(TS)(float)((double)to_f32(src[d]) * sc);
+            s2 += xd * xd;
+          }
+          s2 = wave_sum_f64(s2);
+          const double dev = fabs(sqrt(s2) - 1.0);
+          if (dev < best) { best = dev; best_scale = sc; }
+          if (best <= 6.103515625e-05) break;          // 2^-14: good enough
+        }
+        scale = best_scale;
+      }
+    }
   }
   double ss2 = 0.0, q2 = 0.0;
   TS* dst = out_rows + row * (int64_t)ld;

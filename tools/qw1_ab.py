@@ -18,6 +18,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 SHAPES = {"c2": (10_000_000, 768, "f16", 1024, 32), "c4": (12_500_000, 1024, "bf16", 8192, 64),
+          "c1": (1_000_000, 384, "f16", 256, 10),
           "c2s": (2_000_000, 768, "f16", 1024, 32), "c4s": (2_000_000, 1024, "bf16", 8192, 64)}
 
 
@@ -26,7 +27,8 @@ def main():
     ap.add_argument("--shapes", default="c2,c4")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0,1,2",
+                    help="HCR_OPT_QW1 values, each optionally ':shape' (HCR_OPT_QW1_SHAPE)")
     a = ap.parse_args()
     import hcrag_amd as hc
     dev = torch.device("cuda", 0)
@@ -44,8 +46,10 @@ def main():
         I = torch.empty((B, k), dtype=torch.int64, device=dev)
         ref = None
         for r in range(a.rounds):
-            for v in [int(x) for x in a.variants.split(",")]:
+            for vs in a.variants.split(","):
+                v, shape = (int(x) for x in (vs + ":0").split(":")[:2])
                 ix.set_option(ix.OPT_QW1, v)
+                ix.set_option(ix.OPT_QW1_SHAPE, shape)
                 ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
                 torch.cuda.synchronize()
                 ix.set_timing(True)
@@ -63,13 +67,13 @@ def main():
                 if ref is None:
                     ref = ids
                 fl = 2.0 * B * N * D
-                rec = {"shape": sh, "variant": v, "round": r, "score_kernel": st["score_kernel"],
+                rec = {"shape": sh, "variant": vs, "round": r, "score_kernel": st["score_kernel"],
                        "score_ms": round(min(kms), 4), "score_ms_med": round(sorted(kms)[len(kms) // 2], 4),
                        "wall_ms": round(min(walls), 4), "mfma_frac": round(fl / (min(kms) * 1e-3) / 2.5e15, 4),
-                       "wg": st["workgroups"], "P": st["partitions"], "widened": st["widened_queries"],
+                       "wg": st["workgroups"], "P": st["partitions"], "unit": st["unit_kernel"], "widened": st["widened_queries"],
                        "fallback": st["fallback_queries"], "ids_equal_first": same}
                 print(json.dumps(rec), flush=True)
-                summary.setdefault((sh, v), []).append(min(kms))
+                summary.setdefault((sh, vs), []).append(min(kms))
         ix.close()
         del Q, S, I
         torch.cuda.empty_cache()
