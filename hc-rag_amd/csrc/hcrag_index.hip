@@ -437,6 +437,7 @@ static constexpr int kMergeMaxKeys = 16384;     // keys per merge_lists_kernel b
                                                 // LDS): one level for P x k' <= 256 x 64
 static constexpr int kQueryChunk = 16384;       // queries per pipeline pass (bounds workspace)
 static constexpr int kMaxDevices = 64;          // per-device once-only kernel attributes
+static constexpr size_t kLdsBytes = 160 * 1024;  // LDS per CU (gfx950) = a block's dynamic limit
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
 
@@ -484,6 +485,7 @@ struct TestHooks {
   int qw_min = 0;                    // 0: the measured default (v3_cfg)
   int qw1 = -1;                      // HCR_OPT_QW1 default (-1: the heuristic)
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
+  bool no_finish = false;            // HCRAG_NO_FINISH: separate merge + rescore launches
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -495,6 +497,7 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(5, std::max(-1, atoi(e)));
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
+    t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -703,6 +706,34 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
 }
 
+// Merge of the last <= G lists + rescore in one launch (finish_kernel); false when its LDS
+// (the merge's keys + the fp64 query + the candidates) exceeds the CU's 160 KiB.
+static constexpr size_t kFinishDynLds = kLdsBytes - 4096;   // (its static LDS: the scan, histogram)
+static size_t finish_lds(int np, int kp, int dim) {
+  return (size_t)next_pow2(std::max(np * kp, kp)) * 8 + (size_t)dim * 8 + (size_t)kp * 24 + 16;
+}
+template <typename TS>
+static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, int np, const float* d_q,
+                         int nq, int kp, int k, int mode, double thr, double* out_s, int64_t* out_i,
+                         hipStream_t st) {
+  static std::once_flag lds_once[kMaxDevices];
+  hipError_t lds_err = hipSuccess;
+  std::call_once(lds_once[ix->device], [&] {
+    lds_err = hipFuncSetAttribute((const void*)finish_kernel<TS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kFinishDynLds);
+  });
+  HIPC(lds_err);
+  const int M = next_pow2(std::max(np * kp, kp));
+  hipLaunchKernelGGL((finish_kernel<TS>), dim3(nq), dim3(256), finish_lds(np, kp, ix->dim), st, lists, cnt,
+                     np, M, kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
+                     ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
+                     ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
+                     ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
@@ -754,9 +785,11 @@ seed_from_maxima_kernel(const float* __restrict__ umax, int U, int nqpad, int j,
 // into one sorted top-kp list per query ([q][kp] at the front of w_merged); G lists per block
 // (G x kp <= kMergeMaxKeys: one level for P x kp <= 256 x 64), intermediate levels
 // ping-ponging behind it.
+// With out_cnt / out_p set, the levels stop once at most G lists per query remain (the caller's
+// finish_kernel merges those): *out / *out_cnt / *out_p are then the remaining lists.
 static int merge_groups(int kp) { return std::min(256, std::max(2, kMergeMaxKeys / kp)); }
 static int merge_lists(hcr_index* ix, int nq, int nqpad, int P, int kp, hipStream_t st,
-                       const uint64_t** out) {
+                       const uint64_t** out, const int** out_cnt = nullptr, int* out_p = nullptr) {
   // the dynamic-LDS limit is a per-device attribute: raised once per device, by whichever
   // thread gets there first (hcr_multi_search runs shards of several devices concurrently)
   static std::once_flag lds_once[kMaxDevices];
@@ -776,6 +809,12 @@ static int merge_lists(hcr_index* ix, int nq, int nqpad, int P, int kp, hipStrea
   int* cbufs[2] = {ix->w_mcnt.as<int>(), ix->w_mcnt.as<int>() + (size_t)nqpad * P2};
   int which = 0, pin = P;
   while (true) {
+    if (out_cnt && pin <= G) {
+      *out = src;
+      *out_cnt = cnt;
+      *out_p = pin;
+      return HCR_OK;
+    }
     const int pout = (pin + G - 1) / G;
     const int M = next_pow2(std::min(G, pin) * kp);
     uint64_t* dst = pout == 1 ? final_dst : bufs[which];
@@ -970,12 +1009,29 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   if (ix->timing) HIPC(hipEventRecord(ix->ev1, st));
 
-  CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr));
-
-  if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
-  else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
-  else launch_rescore<float>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
-  HIPC(hipGetLastError());
+  const int* lcnt = nullptr;
+  int lp = 0;
+  CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr, &lcnt, &lp));
+  if (!hooks().no_finish && finish_lds(lp, kp, ix->dim) <= kFinishDynLds) {
+    // the last merge level and K4 in one launch
+    if (ix->dtype == HCR_F16) CHECK(launch_finish<_Float16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
+    else if (ix->dtype == HCR_BF16) CHECK(launch_finish<__bf16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
+    else CHECK(launch_finish<float>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
+  } else {
+    // (lp lists remain: merge them to the single sorted list, then K4)
+    uint64_t* final_dst = ix->w_merged.as<uint64_t>();
+    const int G = merge_groups(kp);
+    if (lp > 1 || merged_ptr != final_dst) {
+      hipLaunchKernelGGL(merge_lists_kernel, dim3(nq, 1), dim3(256), (size_t)next_pow2(std::min(G, lp) * kp) * 8,
+                         st, merged_ptr, lcnt, lp, G, kp, final_dst, (int*)nullptr);
+      HIPC(hipGetLastError());
+    }
+    merged_ptr = final_dst;
+    if (ix->dtype == HCR_F16) launch_rescore<_Float16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+    else if (ix->dtype == HCR_BF16) launch_rescore<__bf16>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+    else launch_rescore<float>(ix, merged_ptr, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st);
+    HIPC(hipGetLastError());
+  }
 
   int cnt = 0;
   HIPC(hipMemcpyAsync(&cnt, ix->w_cnt.p, 4, hipMemcpyDeviceToHost, st));

@@ -47,9 +47,9 @@ bool by_ks(int ks, bool nw8, const QsArgs& a, hipStream_t st) {
 
 // QW1P (score_qw1p.h): 16-row stages in a 6-deep ring at D = 768, 4-deep at D = 1024, 32-row
 // stages 6-deep at D = 384; 3 fragment groups in flight
-template <typename TM, int KS, int SR, int NST>
+template <typename TM, int KS, int SR, int NST, int FD>
 void launch_p(const QsArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk_qw1p_kernel<TM, 256, KS, SR, NST, 3>), dim3(a.nqb * a.P), dim3(QW1_NW * 64),
+  hipLaunchKernelGGL((score_topk_qw1p_kernel<TM, 256, KS, SR, NST, FD>), dim3(a.nqb * a.P), dim3(QW1_NW * 64),
                      0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
                      a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
@@ -57,9 +57,9 @@ template <typename TM>
 bool by_ks_p(int ks, const QsArgs& a, hipStream_t st) {
   if (a.cap != 256) return false;
   switch (ks) {
-    case 12: launch_p<TM, 12, 32, 6>(a, st); return true;
-    case 24: launch_p<TM, 24, 16, 6>(a, st); return true;
-    case 32: launch_p<TM, 32, 16, 4>(a, st); return true;
+    case 12: launch_p<TM, 12, 32, 6, 3>(a, st); return true;
+    case 24: launch_p<TM, 24, 16, 6, 3>(a, st); return true;
+    case 32: launch_p<TM, 32, 16, 4, 4>(a, st); return true;     // (FD must divide NG = 16)
     default: return false;
   }
 }

@@ -41,6 +41,9 @@ score_topk_qw1p_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   constexpr int JE = QB > FD - 1 ? QB : FD - 1;       // the group of the thresholds + appends
   static_assert(D >= 2, "stage s + 1 must be in flight at stage s's barrier");
   static_assert(JE < JB, "the previous stage's epilogue fits before the barrier");
+  // group J reads into av[J % FD], the next stage's group j into av[(NG + j) % FD]: the same
+  // buffer only when FD divides NG (D = 1024: NG = 16, FD = 4)
+  static_assert(NG % FD == 0, "fragment buffers must line up across stages");
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -277,7 +280,7 @@ score_topk_qw1p_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       }
       constexpr int JN = J + FD - 1;
       if constexpr (JN < NG) qw1_issue_frags<goff(JN), OFF2, V>(vcur, av[JN % FD]);
-      else qw1_issue_frags<goff(JN - NG), OFF2, V>(vnext, av[JN % FD]);
+      else qw1_issue_frags<goff(JN - NG), OFF2, V>(vnext, av[JN % FD]);   // (= av[(JN - NG) % FD])
       // LDS reads complete in order: the bounds (issued before group FD-1's fragments) are
       // younger than groups 0 .. FD-2
       if constexpr (J < FD - 1) qw_frag_wait<2 * (FD - 1) + QB>(av[J % FD]);
@@ -327,6 +330,12 @@ score_topk_qw1p_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   }
   // the last stage's epilogue, after its MFMAs (no next stage to hide it in)
   auto drain = [&](floatx4 (&acc)[RB][QB], int sl) __attribute__((always_inline)) {
+    // the last stage read its (nonexistent) successor's first groups: an inline-asm read the
+    // compiler sees no use of frees its VGPRs while the LDS return is pending, so wait for them
+    // with the registers still held (the drain's first registers were overwritten without it)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int f = 0; f < FD; ++f) asm volatile("" : "+v"(av[f][0]), "+v"(av[f][1]));
 #pragma unroll
     for (int m = 0; m < RB; ++m)
 #pragma unroll

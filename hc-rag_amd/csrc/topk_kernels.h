@@ -535,20 +535,14 @@ __device__ inline int block_select_top_u64(uint64_t* a, int c, int kp, int* hist
 // -------------------------------------------------------------------------------------
 // K3: merge the partition survivors of one query into its global top-k' (sorted desc).
 // -------------------------------------------------------------------------------------
-#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 // lists: [q][P][kp] slots, list (q, p) holding cnt[q*P + p] keys (a score kernel's final_list
-// or a previous level).  Block (q, grp) gathers lists [grp*G, grp*G + G) (G <= blockDim) into
-// LDS -- a block scan of their counts places them -- and sorts them: with pout == 1 (the last
-// level) it writes the sorted top-kp, zero padded, to out[q*kp ..]; otherwise the top
-// min(count, kp) to list (q, grp) of the next level, [q][pout][kp] with counts cnt_out.
-__global__ void __launch_bounds__(256)
-merge_lists_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, int P, int G,
-                   int kp, uint64_t* __restrict__ out, int* __restrict__ cnt_out) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t sm_keys[];
-  __shared__ int s_off[257], s_hist[256], s_misc[4];
-  const int q = blockIdx.x, grp = blockIdx.y, pout = gridDim.y;
-  const int p0 = grp * G;
-  const int np = min(G, P - p0);
+// or a previous level).  One block gathers lists [p0, p0 + np) (np <= blockDim) of query q into
+// LDS -- a block scan of their counts places them -- selects and sorts them: on return
+// sm_keys[0, m) is sorted descending (m a power of two >= kp, zero padded) and the count of
+// real keys kept (min(count, kp) are the top of the merge) is returned.
+__device__ __forceinline__ int merge_block_lds(const uint64_t* __restrict__ lists, const int* __restrict__ cnt,
+                                               int P, int p0, int np, int kp, int q, uint64_t* sm_keys,
+                                               int* s_off, int* s_hist, int* s_misc) {
   const int t = threadIdx.x;
   const int c_t = t < np ? min(cnt[(size_t)q * P + p0 + t], kp) : 0;
   // inclusive scan of the counts (Hillis-Steele over the block)
@@ -583,6 +577,22 @@ merge_lists_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ c
   for (int i = cs + t; i < m; i += blockDim.x) sm_keys[i] = 0ull;
   __syncthreads();
   block_sort_desc_u64(sm_keys, m);
+  return cs;
+}
+
+#ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
+// Block (q, grp) merges lists [grp*G, grp*G + G): with pout == 1 (the last level) it writes the
+// sorted top-kp, zero padded, to out[q*kp ..]; otherwise the top min(count, kp) to list
+// (q, grp) of the next level, [q][pout][kp] with counts cnt_out.
+__global__ void __launch_bounds__(256)
+merge_lists_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, int P, int G,
+                   int kp, uint64_t* __restrict__ out, int* __restrict__ cnt_out) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm_keys[];
+  __shared__ int s_off[257], s_hist[256], s_misc[4];
+  const int q = blockIdx.x, grp = blockIdx.y, pout = gridDim.y;
+  const int p0 = grp * G;
+  const int t = threadIdx.x;
+  const int cs = merge_block_lds(lists, cnt, P, p0, min(G, P - p0), kp, q, sm_keys, s_off, s_hist, s_misc);
   if (pout == 1) {
     uint64_t* dst = out + (size_t)q * kp;
     for (int i = t; i < kp; i += blockDim.x) dst[i] = sm_keys[i];
@@ -627,31 +637,25 @@ __device__ __forceinline__ void acc8_f64(double& acc, const TQ* __restrict__ q, 
 // -------------------------------------------------------------------------------------
 // K4: exact fp64 rescoring + certificate + final top-k.
 // -------------------------------------------------------------------------------------
+// The body of K4 for one query (block): `keys` (LDS) holds its merged top-kp coarse keys,
+// sorted descending and zero padded, `qd` (LDS) the fp32 query widened to fp64; hi / lo / nrm
+// are kp-slot LDS arrays.  Writes the query's top-k, its certificate flag and s_k.
 template <typename TS>
-__global__ void __launch_bounds__(256)
-rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restrict__ q32,
-               int dim, const double* __restrict__ qnorm, const double* __restrict__ eps,
-               const TS* __restrict__ rows, int ld, const double* __restrict__ norm64, int k,
-               int mode, double thr, int64_t id_offset, double* __restrict__ out_s,
-               int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
-               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
-               uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap) {
-  extern __shared__ __attribute__((aligned(16))) char sm_raw[];
-  double* qd = reinterpret_cast<double*>(sm_raw);
-  uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
-  uint64_t* lo = hi + kp;
-  uint64_t* keys = lo + kp;
-  double* nrm = reinterpret_cast<double*>(keys + kp);   // candidate row norms
-  int& s_nvalid = *reinterpret_cast<int*>(nrm + kp);    // all LDS in the dynamic region
-  const int q = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* src = q32 + (int64_t)q * dim;
-  for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];
+__device__ __forceinline__ void rescore_block(const uint64_t* keys, const double* qd, uint64_t* hi,
+                                              uint64_t* lo, double* nrm, int* s_nvalid, int q, int kp,
+                                              int dim, const double* __restrict__ qnorm,
+                                              const double* __restrict__ eps, const TS* __restrict__ rows,
+                                              int ld, const double* __restrict__ norm64, int k, int mode,
+                                              double thr, int64_t id_offset, double* __restrict__ out_s,
+                                              int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
+                                              int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
+                                              uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int c = threadIdx.x; c < kp; c += blockDim.x) {   // row norms gathered up front
-    const uint64_t key = merged[(size_t)q * kp + c];
-    keys[c] = key;
+    const uint64_t key = keys[c];
     nrm[c] = key ? norm64[key_row(key)] : 1.0;
   }
-  if (threadIdx.x == 0) s_nvalid = 0;
+  if (threadIdx.x == 0) *s_nvalid = 0;
   __syncthreads();
   const double qn = qnorm[q];
   // RU candidates per wave at a time, their 16-byte row loads in flight together; per
@@ -686,14 +690,14 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
           const uint32_t row = key_row(kk[u]);
           hi[c] = ord64(a / (qn * nrm[c]));
           lo[c] = (uint64_t)(0xFFFFFFFFu - row);
-          atomicAdd(&s_nvalid, 1);
+          atomicAdd(s_nvalid, 1);
         }
       }
     }
   }
   __syncthreads();
   block_sort_desc_pair(hi, lo, kp);
-  const int nvalid = s_nvalid;
+  const int nvalid = *s_nvalid;
   if (threadIdx.x == 0) {
     // Every row outside the candidates has coarse score <= B: the k'-th candidate's coarse
     // score when the list is full, and (estimated seed, tau_est != 0) the seed itself, below
@@ -722,6 +726,60 @@ rescore_kernel(const uint64_t* __restrict__ merged, int kp, const float* __restr
     out_s[(size_t)q * k + t] = s;
     out_i[(size_t)q * k + t] = id;
   }
+}
+
+#define HCR_RESCORE_PARAMS                                                                          \
+  const float *__restrict__ q32, int dim, const double *__restrict__ qnorm,                       \
+      const double *__restrict__ eps, const TS *__restrict__ rows, int ld,                          \
+      const double *__restrict__ norm64, int k, int mode, double thr, int64_t id_offset,            \
+      double *__restrict__ out_s, int64_t *__restrict__ out_i, int *__restrict__ unc_flags,         \
+      int *__restrict__ unc_count, const uint32_t *__restrict__ tau_est,                            \
+      uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap
+#define HCR_RESCORE_ARGS                                                                            \
+  q, kp, dim, qnorm, eps, rows, ld, norm64, k, mode, thr, id_offset, out_s, out_i, unc_flags,      \
+      unc_count, tau_est, sk_out, idmap
+
+// K4 on a merged list ([q][kp] keys in global memory, merge_lists' last level).
+// LDS: dim x 8 (query) + kp x 32 + 16.
+template <typename TS>
+__global__ void __launch_bounds__(256)
+rescore_kernel(const uint64_t* __restrict__ merged, int kp, HCR_RESCORE_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) char sm_raw[];
+  double* qd = reinterpret_cast<double*>(sm_raw);
+  uint64_t* hi = reinterpret_cast<uint64_t*>(sm_raw + (size_t)dim * 8);
+  uint64_t* lo = hi + kp;
+  uint64_t* keys = lo + kp;
+  double* nrm = reinterpret_cast<double*>(keys + kp);
+  int* s_nvalid = reinterpret_cast<int*>(nrm + kp);
+  const int q = blockIdx.x;
+  const float* src = q32 + (int64_t)q * dim;
+  for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];
+  for (int c = threadIdx.x; c < kp; c += blockDim.x) keys[c] = merged[(size_t)q * kp + c];
+  __syncthreads();
+  rescore_block<TS>(keys, qd, hi, lo, nrm, s_nvalid, HCR_RESCORE_ARGS);
+}
+
+// K3 (last merge level) + K4 fused: one block per query merges its P (<= 256) partition lists
+// in LDS and rescores the top kp from there -- no merged list in global memory, one launch and
+// one dependent global round trip fewer per search (fuse merge + rescore).
+// LDS: M x 8 (the merge, M >= next_pow2(P x kp) as merge_lists sizes it) + dim x 8 + kp x 24 + 16.
+template <typename TS>
+__global__ void __launch_bounds__(256)
+finish_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, int P, int M, int kp,
+              HCR_RESCORE_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) char sm_raw[];
+  __shared__ int s_off[257], s_hist[256], s_misc[4];
+  uint64_t* sm_keys = reinterpret_cast<uint64_t*>(sm_raw);
+  double* qd = reinterpret_cast<double*>(sm_keys + M);
+  uint64_t* hi = reinterpret_cast<uint64_t*>(qd + dim);
+  uint64_t* lo = hi + kp;
+  double* nrm = reinterpret_cast<double*>(lo + kp);
+  int* s_nvalid = reinterpret_cast<int*>(nrm + kp);
+  const int q = blockIdx.x;
+  const float* src = q32 + (int64_t)q * dim;
+  for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];   // (under the merge)
+  merge_block_lds(lists, cnt, P, 0, P, kp, q, sm_keys, s_off, s_hist, s_misc);
+  rescore_block<TS>(sm_keys, qd, hi, lo, nrm, s_nvalid, HCR_RESCORE_ARGS);
 }
 
 // -------------------------------------------------------------------------------------
