@@ -24,6 +24,8 @@
 
 #include "encoder_kernels.h"
 #include "gemm_v4.h"
+#define HCR_TOPK_TEMPLATES_ONLY   // (gemm_ws.h reaches topk_kernels.h: its kernels live in hcrag_index.hip)
+#include "gemm_ws.h"
 #include "hcrag.h"
 #include "host_common.h"
 
@@ -53,8 +55,9 @@ struct hcr_encoder {
 static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 // Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
-// forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false; };
+// forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
+// HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -62,6 +65,7 @@ static const EncHooks& enc_hooks() {
     t.ln_scalar = getenv("HCRAG_LN_SCALAR") != nullptr;
     // reference-precision FFN1 GELU with the library erff instead of erf_as
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
+    t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     return t;
   }();
   return h;
@@ -258,12 +262,39 @@ extern "C" int hcr_encoder_finalize(hcr_encoder* e) {
 
 // C = oscale * X . W^T + bias (+ epilogue) on the LDS-DMA ring GEMM (gemm_v4.h).  K is the
 // operand row length (3 x the model width in the reference-precision mode).
+// The weight-stationary GEMM (gemm_ws.h) for 16-bit outputs at K = 384 / 768: nft 256-feature
+// tiles x P token partitions filling one round of 256 workgroups (one per CU: its LDS).
+template <typename TM, int EPI, int KS>
+static void launch_ws_ks(const TM* W, const TM* X, int K, int N, int T, const float* bias, TM* out_h,
+                         int ldo, float oscale, hipStream_t st) {
+  const int sr = ws_sr(KS);
+  const int ntiles = (int)(rup(T, 256) / sr);
+  const int nft = (int)(rup(N, WS_FT) / WS_FT);
+  const int P = std::max(1, std::min(ntiles, 256 / nft));
+  hipLaunchKernelGGL((gemm_ws_kernel<TM, EPI, KS>), dim3((unsigned)(nft * P)), dim3(V3_NT), 0, st, W, X, K, N,
+                     T, nft, P, ntiles, bias, out_h, ldo, oscale);
+}
+template <typename TM, int EPI>
+static bool launch_ws(const TM* W, const TM* X, int K, int N, int T, const float* bias, TM* out_h, int ldo,
+                      float oscale, hipStream_t st) {
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+    if (enc_hooks().no_ws || N > 256 * 64) return false;
+    if (K == 768) { launch_ws_ks<TM, EPI, 24>(W, X, K, N, T, bias, out_h, ldo, oscale, st); return true; }
+    if (K == 384) { launch_ws_ks<TM, EPI, 12>(W, X, K, N, T, bias, out_h, ldo, oscale, st); return true; }
+  }
+  return false;
+}
+
 template <typename TM, int EPI>
 static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const float* bias,
                        const float* resid, TM* out_h, float* out_f, int ldo, float oscale,
                        hipStream_t st) {
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
   if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
+  if (launch_ws<TM, EPI>(W, X, K, N, T, bias, out_h, ldo, oscale, st)) {
+    HIPC(hipGetLastError());
+    return HCR_OK;
+  }
   // feature tile: 192 when it fills the last round of 256-CU workgroups better than 256
   // (N = 768 at T = 32768: 512 tiles = 2 full rounds vs 384 = 1.5); weights are padded to
   // a multiple of 768 rows so either tile reads whole rows.

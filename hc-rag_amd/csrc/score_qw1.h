@@ -408,7 +408,9 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                 if (key > tkr[n]) {
                   const int ql = qle + 16 * n;
                   const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+#ifndef HCR_QW1_NOSTORE   // (diagnostic stamps build only: what the appends' stores cost the ring)
                   wbuf[(size_t)ql * CAP + pos] = key;
+#endif
                   need |= pos + 1 > CAP - SR;
                 }
               }

@@ -659,8 +659,10 @@ __device__ __forceinline__ void rescore_block(const uint64_t* keys, const double
   __syncthreads();
   const double qn = qnorm[q];
   // RU candidates per wave at a time, their 16-byte row loads in flight together; per
-  // candidate the summation order is acc8_f64's (K6's)
-  constexpr int RU = 16;
+  // candidate the summation order is acc8_f64's (K6's).  RU = 8 (r03): ~100 VGPRs, so 4 blocks
+  // per CU are resident and a 1024-query batch is one round of blocks (RU = 16: 183 VGPRs, 2
+  // blocks per CU, two rounds of the block's dependent key -> row -> sort chain)
+  constexpr int RU = 8;
   for (int c0 = wave * RU; c0 < kp; c0 += 4 * RU) {
     uint64_t kk[RU];
     const TS* e[RU];

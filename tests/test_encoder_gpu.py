@@ -266,10 +266,12 @@ def test_from_pretrained_snapshot_dir(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"HCRAG_GEMM_FT": "256"}, {"HCRAG_GEMM_FT": "192", "HCRAG_LN_SCALAR": "1"}])
+@pytest.mark.parametrize("env", [{"HCRAG_GEMM_FT": "256"}, {"HCRAG_GEMM_FT": "192", "HCRAG_LN_SCALAR": "1"},
+                                 {"HCRAG_ENC_NO_WS": "1"}])
 def test_gemm_tile_and_layernorm_variants(env):
-    """The other GEMM feature tile (256 / 192, chosen per shape by wave quantization) and the
-    scalar LayerNorm, forced through their env switches in a child process (read once)."""
+    """The other GEMM feature tile (256 / 192, chosen per shape by wave quantization), the
+    scalar LayerNorm, and the fast modes' QKV / FFN1 on gemm_v4 instead of the weight-stationary
+    gemm_ws, forced through their env switches in a child process (read once)."""
     import os
     import subprocess
     import sys
@@ -279,3 +281,45 @@ def test_gemm_tile_and_layernorm_variants(env):
                         "-k", "tiny_ragged or minilm_shape or cls_pooling"],
                        env=dict(os.environ, **env), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+_WS_CHILD = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1], sys.argv[1] + '/hc-rag_amd']
+import bench, hcrag_amd as hc
+out = {}
+for shape in ("bge-base", "minilm"):
+    cfg = bench.ENC_SHAPES[shape]
+    for mode in ("f16", "bf16"):
+        enc = hc.BertEncoder(cfg, bench.random_bert_state(cfg, seed=3), dtype=mode, device=0)
+        ids, mask = bench.enc_inputs(cfg, 300, 32, torch.device("cuda", 0), 9)
+        o = torch.empty((300, cfg["hidden"]), dtype=torch.float32, device="cuda:0")
+        enc.encode_device(ids, mask, o, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        out[shape + "_" + mode] = o.cpu().numpy()
+np.savez(sys.argv[2], **out)
+"""
+
+
+@pytest.mark.gpu
+def test_ws_gemm_matches_v4(tmp_path):
+    """gemm_ws (weights in VGPRs, tokens streamed; the fast modes' K = 768 / 384 QKV and FFN1)
+    against gemm_v4 (HCRAG_ENC_NO_WS) over a whole bge-base and MiniLM forward (300 ragged
+    sequences: a partial last token tile) in f16 and bf16.  Same k order and epilogue
+    arithmetic: the embeddings agree to fp32 rounding."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for env in ({}, {"HCRAG_ENC_NO_WS": "1"}):
+        f = str(tmp_path / f"ws{len(res)}.npz")
+        e = dict(os.environ, **env)
+        if not env:
+            e.pop("HCRAG_ENC_NO_WS", None)
+        subprocess.run([sys.executable, "-c", _WS_CHILD, root, f], env=e, check=True, timeout=300)
+        res.append(np.load(f))
+    for key in res[0].files:
+        a, b = res[0][key], res[1][key]
+        assert np.isfinite(a).all(), key
+        np.testing.assert_allclose(a, b, rtol=0, atol=2e-6, err_msg=key)
