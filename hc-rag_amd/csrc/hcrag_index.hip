@@ -60,7 +60,7 @@ struct hcr_index {
       w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
-      f_hcnt, f_hmin;
+      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
@@ -136,7 +136,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
-                   &ix->f_hcnt, &ix->f_hmin};
+                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp};
   for (DevBuf* b : all) b->release();
   if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
@@ -486,6 +486,7 @@ struct TestHooks {
   int qw1 = -1;                      // HCR_OPT_QW1 default (-1: the heuristic)
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
   bool no_finish = false;            // HCRAG_NO_FINISH: separate merge + rescore launches
+  bool no_mfma_filter = false;       // HCRAG_NO_MFMA_FILTER: the fallback's scans on K6 (fp64 only)
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -498,6 +499,7 @@ static const TestHooks& hooks() {
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
+    t.no_mfma_filter = getenv("HCRAG_NO_MFMA_FILTER") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -709,6 +711,7 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
 // Merge of the last <= G lists + rescore in one launch (finish_kernel); false when its LDS
 // (the merge's keys + the fp64 query + the candidates) exceeds the CU's 160 KiB.
 static constexpr size_t kFinishDynLds = kLdsBytes - 4096;   // (its static LDS: the scan, histogram)
+static constexpr int kFinishMaxQueries = 512;
 static size_t finish_lds(int np, int kp, int dim) {
   return (size_t)next_pow2(std::max(np * kp, kp)) * 8 + (size_t)dim * 8 + (size_t)kp * 24 + 16;
 }
@@ -839,6 +842,35 @@ static size_t merge_workspace_keys(int nqpad, int P, int kp) {
   return (size_t)nqpad * kp * (1 + (P2 > 1 ? 2 * P2 : 0));
 }
 
+// The corpus' norm statistics (rho, unit deviation): recomputed after an add.
+static int refresh_norm_stats(hcr_index* ix) {
+  if (!ix->rho_dirty) return HCR_OK;
+  unsigned int rho_bits = 0;
+  HIPC(hipStreamSynchronize(ix->stream));
+  HIPC(hipMemcpy(&rho_bits, ix->rho.p, 4, hipMemcpyDeviceToHost));
+  float rho_f;
+  memcpy(&rho_f, &rho_bits, 4);
+  ix->rho_host = (double)rho_f;
+  unsigned long long* ud = reinterpret_cast<unsigned long long*>(ix->rho.as<char>() + 8);
+  HIPC(hipMemsetAsync(ud, 0, 8, ix->stream));
+  hipLaunchKernelGGL(unit_dev_kernel, dim3(1024), dim3(256), 0, ix->stream, ix->inv32.as<const float>(),
+                     ix->n, ud);
+  HIPC(hipGetLastError());
+  unsigned long long ud_bits = 0;
+  HIPC(hipStreamSynchronize(ix->stream));
+  HIPC(hipMemcpy(&ud_bits, ud, 8, hipMemcpyDeviceToHost));
+  memcpy(&ix->unit_dev_host, &ud_bits, 8);
+  ix->rho_dirty = false;
+  return HCR_OK;
+}
+
+// rigorous fp32 accumulation bound of a K-deep MFMA dot: gamma_{ld+1} + 4u (u = 2^-24)
+static double accum_gamma(int ld) {
+  const double u = std::ldexp(1.0, -24);
+  const double nu = (ld + 1) * u;
+  return nu / (1.0 - nu) + 4.0 * u;
+}
+
 // One pipeline pass over nq (<= kQueryChunk) device queries at candidate depth kp.
 // Returns the number of uncertified queries in *n_unc (stream is synchronised).
 static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode, double thr,
@@ -848,25 +880,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // kernel choice: v3/v4 (deep LDS-DMA ring, tile shape by batch size) for 16-bit rows;
   // v1 (register-staged 128 x 128, converts fp32 rows to bf16 on the way into LDS) for fp32
   // rows and for rows too narrow for the v3 tile-slot rings.
-  // the corpus' norm statistics (rho, unit deviation): recomputed after an add
-  if (ix->rho_dirty) {
-    unsigned int rho_bits = 0;
-    HIPC(hipStreamSynchronize(ix->stream));
-    HIPC(hipMemcpy(&rho_bits, ix->rho.p, 4, hipMemcpyDeviceToHost));
-    float rho_f;
-    memcpy(&rho_f, &rho_bits, 4);
-    ix->rho_host = (double)rho_f;
-    unsigned long long* ud = reinterpret_cast<unsigned long long*>(ix->rho.as<char>() + 8);
-    HIPC(hipMemsetAsync(ud, 0, 8, ix->stream));
-    hipLaunchKernelGGL(unit_dev_kernel, dim3(1024), dim3(256), 0, ix->stream,
-                       ix->inv32.as<const float>(), ix->n, ud);
-    HIPC(hipGetLastError());
-    unsigned long long ud_bits = 0;
-    HIPC(hipStreamSynchronize(ix->stream));
-    HIPC(hipMemcpy(&ud_bits, ud, 8, hipMemcpyDeviceToHost));
-    memcpy(&ix->unit_dev_host, &ud_bits, 8);
-    ix->rho_dirty = false;
-  }
+  CHECK(refresh_norm_stats(ix));
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
                           qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
@@ -915,10 +929,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   // (q^ = 0, every score 0) get the bound ord32(+inf): with bound 0 they passed the epilogue's
   // tile test on every tile and sent their waves down the exact path (r01g).)
 
-  // rigorous accumulation bound: gamma_{ld+1} + 4u (u = 2^-24)
-  const double u = std::ldexp(1.0, -24);
-  const double nu = (ix->ld + 1) * u;
-  const double gamma_u = nu / (1.0 - nu) + 4.0 * u;
+  const double gamma_u = accum_gamma(ix->ld);
   const double rho = ix->rho_host;
   // UNIT score kernels (raw dot product as the coarse score) for L2-normalised corpora; the
   // certificate bound grows by (1+eps)(1+u)(unit_dev + u)
@@ -1012,7 +1023,10 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int* lcnt = nullptr;
   int lp = 0;
   CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr, &lcnt, &lp));
-  if (!hooks().no_finish && finish_lds(lp, kp, ix->dim) <= kFinishDynLds) {
+  // fused for small batches (configs[1], B = 256: 0.372 vs 0.376 ms per search); above
+  // kFinishMaxQueries the separate launches (W = 8 rank shape, B = 1024: 1.973-1.985 vs
+  // 1.985-1.998 ms: the fused block's merge LDS cuts the rescore's residency; r03f A/B)
+  if (!hooks().no_finish && nq <= kFinishMaxQueries && finish_lds(lp, kp, ix->dim) <= kFinishDynLds) {
     // the last merge level and K4 in one launch
     if (ix->dtype == HCR_F16) CHECK(launch_finish<_Float16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
     else if (ix->dtype == HCR_BF16) CHECK(launch_finish<__bf16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
@@ -1074,6 +1088,33 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   const size_t sel_lds = (size_t)2 * cap * 8;
   HIPC(hipFuncSetAttribute((const void*)exact_select_kernel,
                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+  // the MFMA prefilter (K6m, and K6h for queries without a starting threshold) for 16-bit rows
+  // at ld = 384 / 768 / 1024; K6 (an fp64 dot per row and query) otherwise
+  const int ksteps = ix->ld / 32;
+  const bool mf = ix->dtype != HCR_F32 && (ksteps == 12 || ksteps == 24 || ksteps == 32) &&
+                  !hooks().no_mfma_filter;
+  if (mf) CHECK(refresh_norm_stats(ix));
+  const unsigned mgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32, 2048));
+#define MFIL(TS, KS, HIST)                                                                        \
+  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, HIST>), dim3(mgrid), dim3(256), 0, st,     \
+                     ix->f_qhat.as<const TS>(), ix->f_eps.as<const double>(), ix->f_q.as<const float>(), \
+                     ng, ix->dim, ix->f_qn.as<const double>(), ix->rows.as<const TS>(), ix->ld, ix->n, \
+                     ix->inv32.as<const float>(), ix->norm64.as<const double>(),                 \
+                     ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr,                \
+                     ix->f_thh.as<const uint64_t>(), ix->f_thl.as<const uint64_t>(),            \
+                     ix->f_act.as<const int>(), cap, ix->f_cnt.as<unsigned int>(),               \
+                     ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
+                     ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
+                     ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>(),        \
+                     ix->f_ch.as<unsigned int>())
+#define MFIL_KS(TS, HIST)                                                                         \
+  do {                                                                                            \
+    if (ksteps == 12) MFIL(TS, 12, HIST); else if (ksteps == 24) MFIL(TS, 24, HIST); else MFIL(TS, 32, HIST); \
+  } while (0)
+  auto launch_mfil = [&](int ng, bool hist) {
+    if (ix->dtype == HCR_F16) { if (hist) MFIL_KS(_Float16, true); else MFIL_KS(_Float16, false); }
+    else { if (hist) MFIL_KS(__bf16, true); else MFIL_KS(__bf16, false); }
+  };
   for (size_t g0 = 0; g0 < idx.size(); g0 += kFallbackGroup) {
     const int ng = (int)std::min<size_t>(kFallbackGroup, idx.size() - g0);
     CHECK(ix->f_idx.ensure((size_t)ng * 4));
@@ -1113,6 +1154,57 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
                        ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
     HIPC(hipGetLastError());
+    if (mf) {
+      // the group's unit MFMA-dtype queries and eps_q for the non-UNIT coarse score c =
+      // fl(q^.e . inv32); padded to kFallbackGroup with zero queries
+      CHECK(ix->f_qhat.ensure((size_t)kFallbackGroup * ix->ld * 2));
+      CHECK(ix->f_eps.ensure((size_t)kFallbackGroup * 8));
+      CHECK(ix->f_tmp.ensure(1024));
+      char* tmp = ix->f_tmp.as<char>();
+#define PREP(TM)                                                                                   \
+  hipLaunchKernelGGL((prep_queries_kernel<TM>), dim3((kFallbackGroup + 3) / 4), dim3(256), 0, st,     \
+                     ix->f_q.as<const float>(), ng, kFallbackGroup, ix->dim, ix->ld, ix->f_qhat.as<TM>(), \
+                     reinterpret_cast<double*>(tmp), ix->f_eps.as<double>(), ix->rho_host,            \
+                     accum_gamma(ix->ld), -1.0, reinterpret_cast<uint32_t*>(tmp + 256),              \
+                     reinterpret_cast<uint32_t*>(tmp + 384), reinterpret_cast<int*>(tmp + 512))
+      if (ix->dtype == HCR_F16) PREP(_Float16); else PREP(__bf16);
+#undef PREP
+      HIPC(hipGetLastError());
+      bool need0 = false;
+      for (int i = 0; i < ng; ++i) need0 |= thh[i] == 0ull;
+      if (need0) {
+        // round 0 (K6h): coarse histograms -> a starting threshold T_q <= the true k-th best
+        CHECK(ix->f_ch.ensure((size_t)kFallbackGroup * kFbHistBins * 4));
+        HIPC(hipMemsetAsync(ix->f_ch.p, 0, (size_t)ng * kFbHistBins * 4, st));
+        launch_mfil(ng, true);
+        HIPC(hipGetLastError());
+        std::vector<unsigned int> hist((size_t)ng * kFbHistBins);
+        std::vector<double> epsq(ng);
+        HIPC(hipMemcpyAsync(hist.data(), ix->f_ch.p, hist.size() * 4, hipMemcpyDeviceToHost, st));
+        HIPC(hipMemcpyAsync(epsq.data(), ix->f_eps.p, (size_t)ng * 8, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        const double bw = 2.0 * kFbHistRange / kFbHistBins;
+        for (int i = 0; i < ng; ++i) {
+          if (thh[i] != 0ull || epsq[i] < 0.0) continue;    // (eps < 0: zero query, all scores 0)
+          uint64_t acc = 0;
+          for (int b = kFbHistBins - 1; b >= 0; --b) {
+            acc += hist[(size_t)i * kFbHistBins + b];
+            if (acc >= (uint64_t)k) {
+              // >= k rows have c >= edge (less the float binning's rounding), so exact >= T
+              const double T = (-kFbHistRange + b * bw) - 1e-5 - epsq[i];
+              uint64_t u;
+              memcpy(&u, &T, 8);
+              thh[i] = u ^ ((u >> 63) ? 0xFFFFFFFFFFFFFFFFull : 0x8000000000000000ull);   // ord64
+              hlo[i] = T;
+              break;
+            }
+          }
+        }
+        HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(ix->f_hlo.p, hlo.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+        ix->stats.fallback_rounds += 1;
+      }
+    }
     // (one histogram flush per block: 2048 blocks x 4 waves, ~1.2k rows per wave at 10M rows)
     const unsigned fgrid = (unsigned)std::min<int64_t>((ix->n + 3) / 4, 2048);
     int again = 1, rounds = 0;
@@ -1133,7 +1225,8 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>())
-      if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
+      if (mf) launch_mfil(ng, false);
+      else if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
 #undef FIL
       hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
                          ix->f_cnt.as<const unsigned int>(), ix->f_bufh.as<const uint64_t>(),
@@ -1149,6 +1242,8 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     }
     ix->stats.fallback_rounds += rounds;
   }
+#undef MFIL_KS
+#undef MFIL
   return HCR_OK;
 }
 

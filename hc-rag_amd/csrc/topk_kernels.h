@@ -890,6 +890,169 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
   }
 }
 
+// -------------------------------------------------------------------------------------
+// K6m / K6h: the exact fallback's row scan with an MFMA prefilter (16-bit storage, ld = 32 KS).
+//   A group of <= kFbGroup queries is held as MFMA B fragments (q^ = the unit MFMA-dtype
+//   queries of prep_queries_kernel, 16 per wave: waves 0 / 2 queries 0-15, 1 / 3 queries
+//   16-31), rows stream straight from HBM as A fragments, 16-row tiles; the coarse score is
+//   c = fl(q^.e . inv32) with |c - exact| <= eps_q (the non-UNIT bound).
+//   K6m (HIST = false): a (row, query) pair whose c reaches T_q - eps_q -- T_q the score of the
+//   query's threshold key -- gets the fp64 cosine in K6's summation order (a wave per pair:
+//   bit-identical scores), then K6's key test, append and histogram; every row whose exact key
+//   is at or above the threshold passes the prefilter, so K7 sees what K6 would have admitted.
+//   K6h (HIST = true, round 0 when a query has no starting threshold, k > 256): a histogram of
+//   c per query over [-kFbHistRange, kFbHistRange) in kFbHistBins bins, from which the host
+//   takes T_q = (lower edge of the bin where k rows are reached from the top) - eps_q: at least
+//   k rows have c >= edge, hence exact >= T_q, so T_q <= the true k-th best.
+// -------------------------------------------------------------------------------------
+constexpr int kFbHistBins = 512;
+constexpr float kFbHistRange = 1.0625f;
+
+template <typename TS, int KS, bool HIST>
+__global__ void __launch_bounds__(256)
+exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__ eps,
+                         const float* __restrict__ q32, int nq, int dim,
+                         const double* __restrict__ qnorm, const TS* __restrict__ rows, int ld,
+                         int64_t n, const float* __restrict__ inv32,
+                         const double* __restrict__ norm64, const uint32_t* __restrict__ maskbits,
+                         const uint64_t* __restrict__ th_hi, const uint64_t* __restrict__ th_lo,
+                         const int* __restrict__ active, int cap, unsigned int* __restrict__ cnt,
+                         uint64_t* __restrict__ buf_hi, uint64_t* __restrict__ buf_lo,
+                         const double* __restrict__ h_lo, const double* __restrict__ h_hi,
+                         unsigned int* __restrict__ h_cnt, unsigned long long* __restrict__ h_min,
+                         unsigned int* __restrict__ c_hist) {
+  using Op = MfmaOp<TS>;
+  using V = typename Op::V;
+  constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
+  constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
+  __shared__ __attribute__((aligned(16))) char sm[HB > FB ? HB : FB];
+  __shared__ double s_tc[kFbGroup];
+  unsigned int* s_hist = reinterpret_cast<unsigned int*>(sm);                        // HIST
+  unsigned int (*s_cnt)[kFbBins + 1] = reinterpret_cast<unsigned int (*)[kFbBins + 1]>(sm);
+  unsigned long long (*s_min)[kFbBins + 1] =
+      reinterpret_cast<unsigned long long (*)[kFbBins + 1]>(sm + (size_t)kFbGroup * (kFbBins + 1) * 4);
+  if constexpr (HIST) {
+    for (int i = threadIdx.x; i < kFbGroup * kFbHistBins; i += blockDim.x) s_hist[i] = 0u;
+  } else {
+    for (int i = threadIdx.x; i < kFbGroup * (kFbBins + 1); i += blockDim.x) {
+      (&s_cnt[0][0])[i] = 0u;
+      (&s_min[0][0])[i] = ~0ull;
+    }
+    if (threadIdx.x < kFbGroup) {
+      const int q = threadIdx.x;
+      // the prefilter bound: pairs below it cannot reach the threshold key's score
+      s_tc[q] = (q < nq && active[q]) ? unord64(th_hi[q]) - eps[q] : INFINITY;
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qb = wave & 1;
+  const int ql = qb * 16 + (lane & 15);              // the lane's query (accumulator column)
+  // query fragments: lane l holds q^[qb*16 + (l & 15)][32 ks + 8 (l >> 4) .. + 8)
+  V qf[KS];
+  {
+    const TS* src = qhat + (size_t)ql * ld + (lane >> 4) * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
+  }
+  const bool qok = ql < nq && active[ql];
+  const double tcq = HIST ? 0.0 : s_tc[ql];
+  const int64_t ntile = (n + 15) / 16;
+  const int64_t stride = (int64_t)gridDim.x * 2;
+  for (int64_t t = (int64_t)blockIdx.x * 2 + (wave >> 1); t < ntile; t += stride) {
+    const int64_t r0 = t * 16;
+    // A fragments straight from the rows (the slack rows past n are readable; masked below)
+    const TS* ra = rows + (r0 + (lane & 15)) * ld + (lane >> 4) * 8;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    constexpr int CH = 8;                            // k-steps per batch of loads in flight
+#pragma unroll
+    for (int k0 = 0; k0 < KS; k0 += CH) {
+      V a[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (k0 + j < KS) a[j] = *reinterpret_cast<const V*>(ra + (k0 + j) * 32);
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (k0 + j < KS) acc = Op::run(a[j], qf[k0 + j], acc);
+    }
+    const int64_t rb = r0 + (lane >> 4) * 4;         // the lane's 4 rows: rb .. rb + 3
+    float iv[4];
+    bool rok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = rb + r;
+      rok[r] = qok && row < n && (!maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u));
+      iv[r] = row < n ? inv32[row] : 0.f;
+    }
+    if constexpr (HIST) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!rok[r]) continue;
+        const float c = acc[r] * iv[r];
+        int b = (int)floorf((c + kFbHistRange) * ((float)kFbHistBins / (2.f * kFbHistRange)));
+        b = b < 0 ? 0 : b >= kFbHistBins ? kFbHistBins - 1 : b;
+        atomicAdd(&s_hist[ql * kFbHistBins + b], 1u);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bool adm = rok[r] && (double)(acc[r] * iv[r]) >= tcq;
+        uint64_t m = __builtin_amdgcn_ballot_w64(adm);
+        while (m) {                                  // a wave per admitted pair (rare)
+          const int src = __builtin_ctzll(m);
+          m &= m - 1;
+          const int q = __builtin_amdgcn_readlane(ql, src);
+          const int64_t row = rb - (lane >> 4) * 4 + (src >> 4) * 4 + r;
+          const TS* e = rows + row * ld;
+          const float* qs = q32 + (int64_t)q * dim;
+          double ex = 0.0;
+          for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+            float x[8];
+            load8_f32(e + d0, x);
+            acc8_f64(ex, qs, d0, dim, x);
+          }
+          ex = wave_sum_f64(ex);
+          if (lane == 0) {
+            const double sc = ex / (qnorm[q] * norm64[row]);
+            const uint64_t h = ord64(sc);
+            const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)row);
+            if (h > th_hi[q] || (h == th_hi[q] && l >= th_lo[q])) {
+              const unsigned int p = atomicAdd(&cnt[q], 1u);
+              if (p < (unsigned int)cap) {
+                buf_hi[(size_t)q * cap + p] = h;
+                buf_lo[(size_t)q * cap + p] = l;
+              }
+              const double lo = h_lo[q], hi = h_hi[q];
+              int b = kFbBins;
+              if (sc < hi) {
+                const double tt = (sc - lo) * ((double)kFbBins / (hi - lo));
+                b = tt < 0.0 ? 0 : tt >= (double)(kFbBins - 1) ? kFbBins - 1 : (int)tt;
+              }
+              atomicAdd(&s_cnt[q][b], 1u);
+              atomicMin(&s_min[q][b], (unsigned long long)h);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (HIST) {
+    for (int i = threadIdx.x; i < nq * kFbHistBins; i += blockDim.x) {
+      const unsigned int c = s_hist[i];
+      if (c) atomicAdd(&c_hist[i], c);
+    }
+  } else {
+    for (int i = threadIdx.x; i < nq * (kFbBins + 1); i += blockDim.x) {
+      const unsigned int c = (&s_cnt[0][0])[i];
+      if (c) {
+        atomicAdd(&h_cnt[i], c);
+        atomicMin(&h_min[i], (&s_min[0][0])[i]);
+      }
+    }
+  }
+}
+
 #ifndef HCR_TOPK_TEMPLATES_ONLY   // defined once (hcrag_index.hip): one registration per kernel
 __global__ void __launch_bounds__(256)
 exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,

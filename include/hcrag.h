@@ -141,12 +141,14 @@ typedef struct {
   int32_t unit_kernel;        /* 1: the UNIT score kernel ran (L2-normalised corpus, raw dot
                                  product as coarse score, widened certificate bound) */
   int32_t fallback_queries;   /* queries answered by the exact fp64 scan (K6/K7) */
-  int32_t fallback_rounds;    /* K6/K7 rounds run (threshold tightenings + 1 per group) */
+  int32_t fallback_rounds;    /* K6/K7 rounds run (threshold tightenings + 1 per group; + the
+                                 MFMA prefilter's round-0 histogram where it ran) */
   int32_t score_kernel;       /* dense score kernel of the first pass: 1 register-staged
                                  128 x 128 (fp32 rows), 3 v3 (256 x 16 / 256 x 64), 4 v4
                                  (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW,
                                  7 QW1 (one wave per SIMD, 64 / 48 queries per wave),
-                                 8 QW1 in its 8-wave form (D = 384: two row halves per query set) */
+                                 8 QW1 in its 8-wave form (D = 384: two row halves per query set),
+                                 9 QW1P (QW1 software-pipelined, HCR_OPT_QW1 = 5) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
@@ -157,7 +159,8 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *   HCR_OPT_QW1: large-batch kernel at D = 384 / 768 / 1024.  -1 = default heuristic, 0 = never
  *                QW1 (D = 384: QS, D = 768: QW, D = 1024: v4), 1 = QW1 with its DMA issue spread
  *                over the MFMA groups, 2 = QW1 with the DMA issue at the stage barrier, 3 / 4 = the
- *                same with the 8-wave form where it exists (D = 384), else as 1 / 2.
+ *                same with the 8-wave form where it exists (D = 384), else as 1 / 2, 5 = QW1P (QW1
+ *                software-pipelined: the previous stage's epilogue under the MFMAs).
  *   HCR_OPT_QW1_SHAPE: QW1's stage shape at D = 768 (tuning): 0 = 32-row stages, 3-deep ring,
  *                3 fragment groups in flight; 1 = 4 groups in flight; 2 = 16-row stages, 6-deep
  *                ring; 3 = both. */

@@ -305,8 +305,11 @@ np.savez(sys.argv[2], **out)
 def test_ws_gemm_matches_v4(tmp_path):
     """gemm_ws (weights in VGPRs, tokens streamed; the fast modes' K = 768 / 384 QKV and FFN1)
     against gemm_v4 (HCRAG_ENC_NO_WS) over a whole bge-base and MiniLM forward (300 ragged
-    sequences: a partial last token tile) in f16 and bf16.  Same k order and epilogue
-    arithmetic: the embeddings agree to fp32 rounding."""
+    sequences: a partial last token tile) in f16 and bf16.  The W fragments are the A operand
+    in WS (C^T tiles) and the B operand in v4, so the fp32 sums round differently and 12
+    layers of 16-bit activations carry that to ~1e-4 (r03 box: max 7.9e-5); both are checked
+    against the fp32 HF model elsewhere (test_bge_shapes_cls on WS, env2 above on v4).  Here:
+    within the fast modes' documented envelope of each other, cosine >= 0.99999 per row."""
     import os
     import subprocess
     import sys
@@ -322,4 +325,6 @@ def test_ws_gemm_matches_v4(tmp_path):
     for key in res[0].files:
         a, b = res[0][key], res[1][key]
         assert np.isfinite(a).all(), key
-        np.testing.assert_allclose(a, b, rtol=0, atol=2e-6, err_msg=key)
+        np.testing.assert_allclose(a, b, rtol=0, atol=5e-4, err_msg=key)
+        cos = (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+        assert cos.min() >= 0.99999, (key, cos.min())

@@ -88,6 +88,70 @@ def test_large_k_exact_scan(hc):
             ix.search(Q, 2049)
 
 
+@pytest.mark.parametrize("D", [384, 768, 1024])
+def test_large_k_mfma_prefilter(hc, D):
+    """k > 256 on the MFMA prefilter (K6h round-0 coarse histograms -> starting threshold, then
+    K6m: fp64 only for rows whose coarse score reaches threshold - eps): raw (non-normalised)
+    rows, 2 query groups (32 + 9), a row mask and a threshold; ids identical to the oracle,
+    scores to 1e-12.  A near-duplicate cluster of 3000 rows around one query forces overflow
+    rounds (its k = 2048 best lie inside one coarse bin)."""
+    rng = np.random.default_rng(D + 7)
+    N, B = 60000 + 7, 41
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    E[:3000] = E[0] + 1e-3 * rng.standard_normal((3000, D)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[0] = E[0]
+    mask = rng.random(N) < 0.7
+    with hc.VectorIndex(D, "bf16" if D == 1024 else "f16") as ix:
+        ix.add(E, normalize=False)
+        R = ix.get_rows()
+        for k in (257, 2048):
+            s, i = ix.search(Q, k)
+            es, ei = O.cosine_topk(Q, R, k)
+            _check(s, i, es, ei)
+            st = ix.last_stats()
+            assert st["fallback_queries"] == B, st
+        ix.set_rowmask(mask)
+        s, i = ix.search(Q[:9], 700, threshold=0.02)
+        es, ei = O.cosine_topk(Q[:9], R, 700, threshold=0.02, rowmask=mask)
+        _check(s, i, es, ei)
+
+
+_PF_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[1] + '/hc-rag_amd']
+import hcrag_amd as hc
+rng = np.random.default_rng(5)
+N, D = 200000 + 3, 768
+E = rng.standard_normal((N, D)).astype(np.float32)
+Q = rng.standard_normal((40, D)).astype(np.float32)
+with hc.VectorIndex(D, "f16") as ix:
+    ix.add(E, normalize=True)
+    s, i = ix.search(Q, 1500)
+    st = ix.last_stats()
+np.savez(sys.argv[2], s=s, i=i, rounds=st["fallback_rounds"])
+"""
+
+
+def test_mfma_prefilter_matches_fp64_scan(tmp_path):
+    """The prefiltered scan (default) and K6's fp64 scan of every row (HCRAG_NO_MFMA_FILTER)
+    return bit-identical lists: the admitted rows' scores are computed in K6's order."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = []
+    for env in ({}, {"HCRAG_NO_MFMA_FILTER": "1"}):
+        e = dict(os.environ, **env)
+        if not env:
+            e.pop("HCRAG_NO_MFMA_FILTER", None)
+        f = str(tmp_path / f"pf{len(out)}.npz")
+        subprocess.run([sys.executable, "-c", _PF_CHILD, root, f], env=e, check=True, timeout=300)
+        out.append(np.load(f))
+    np.testing.assert_array_equal(out[0]["i"], out[1]["i"])
+    np.testing.assert_array_equal(out[0]["s"], out[1]["s"])
+
+
 def test_large_k_sorted_corpus_converges(hc):
     """a corpus ordered by ascending score against the query (the scan admits the
     worst rows first).  K7's histogram threshold does not depend on admission order, so the

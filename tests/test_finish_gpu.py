@@ -1,9 +1,10 @@
 """The fused last-merge-level + rescore kernel (finish_kernel, topk_kernels.h) against the separate
 merge_lists_kernel + rescore_kernel launches (HCRAG_NO_FINISH, run in a child process): results
 must be bit-identical (same keys, same fp64 summation order), and both equal to the fp64 oracle.
-Shapes: configs[1]'s QS batch (P = 256 lists of k' = 64: one 16384-key level), the QW batch with
-a multi-level merge (k' = 512 after widening: G = 32 lists per level), and QW1's 8-wave form
-(two final lists per partition).  Reference: experiments/main.py:841-844."""
+Shapes: configs[1]'s QS batch (P = 256 lists of k' = 64: one 16384-key level), a QW batch with
+a multi-level merge (k' = 512: G = 32 lists per level), and QW1's 8-wave form (two final lists
+per partition); all <= 512 queries (kFinishMaxQueries: larger batches take the separate
+launches).  Reference: experiments/main.py:841-844."""
 import os
 import subprocess
 import sys
@@ -16,7 +17,7 @@ from oracle import cosine_topk as O
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = [(384, 150_000 + 77, 256, 10, -1), (768, 60_000 + 5, 1024, 200, -1), (384, 80_000 + 1, 512, 32, 3)]
+CASES = [(384, 150_000 + 77, 256, 10, -1), (768, 60_000 + 5, 512, 200, -1), (384, 80_000 + 1, 512, 32, 3)]
 
 _CHILD = r"""
 import sys, numpy as np

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 T=tools/gpu_step.sh
 E="python bench.py --rows 200000 --encoder bge-base --enc-modes f32,f16 --no-cpu-baseline --no-configs0 --no-configs1 --no-configs4 --sweep , --pipe-modes , --steps 5 --warmup 2"
 W8="python bench.py --encoder none --no-cpu-baseline --no-configs0 --no-configs1 --no-configs4 --sweep , --steps 30 --warmup 3 --rows 1250000"
-$T r03g_enc_tests 900 python -u -m pytest tests/test_encoder_gpu.py -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider && \
+$T r03g_enc_tests 900 python -u -m pytest tests/test_exact_gpu.py tests/test_encoder_gpu.py -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider && \
 $T r03g_enc_ws 300 $E && \
 HCRAG_ENC_NO_WS=1 $T r03g_enc_v4 300 $E && \
 $T r03g_enc_ws2 300 $E && \
