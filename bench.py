@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--pipe-steps", type=int, default=5)
     p.add_argument("--no-configs1", action="store_true",
                    help="skip the configs[1] leg (1M x 384 f16, B = 256, top-10; 1 GPU)")
+    p.add_argument("--no-vendor-gemm", action="store_true",
+                   help="skip the vendor-GEMM calibration of the MFMA roofline (torch.mm)")
     p.add_argument("--no-configs4", action="store_true",
                    help="skip the configs[4] per-rank leg (12.5M x 1024 bf16, 8192 queries, "
                         "top-64, bge-large encoder; 1 GPU)")
@@ -300,6 +302,41 @@ def pipeline_leg(a, hc, dev, rank, world, dist, searcher, B, nq, mode):
             "search_ms": round((per - enc_only) * 1e3, 3),
             "path": "token ids -> encoder -> all-gather -> certified top-k -> all-to-all -> merge"
                     if world > 1 else "token ids -> encoder -> certified top-k (one stream)"}
+
+
+def vendor_gemm_leg(dev, seconds=2.0):
+    """What the chip sustains on plain fp16 GEMMs through the vendor library (torch.mm ->
+    hipBLASLt / rocBLAS), on random operands, after a warm-up long enough for the clock to
+    settle under load (MI355X_MICROARCH.md 'DVFS give-back'): the headline's GEMM shape without
+    the top-k (1024 queries x 768 . 768 x 131072-row chunks, fp16 out) and a square 8192^3.
+    A calibration of the MFMA roofline under the power and clock the board holds; not a
+    baseline of the retrieval path (the dense kernel also selects its top-k')."""
+    out = {}
+    for name, (M, Nn, K) in {"headline_shape_1024x131072x768": (1024, 131072, 768),
+                             "square_8192": (8192, 8192, 8192)}.items():
+        A = torch.randn((M, K), device=dev, dtype=torch.float16)
+        B = torch.randn((Nn, K), device=dev, dtype=torch.float16)
+        C = torch.empty((M, Nn), device=dev, dtype=torch.float16)
+        t_end = time.perf_counter() + seconds / 2            # warm-up: the clock settles
+        while time.perf_counter() < t_end:
+            torch.mm(A, B.t(), out=C)
+            torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n, ms = 0, 0.0
+        while ms < seconds * 500:
+            e0.record()
+            for _ in range(8):
+                torch.mm(A, B.t(), out=C)
+            e1.record()
+            e1.synchronize()
+            ms += e0.elapsed_time(e1)
+            n += 8
+        tf = 2.0 * M * Nn * K * n / (ms * 1e-3) / 1e12
+        out[name] = {"TFLOPs": round(tf, 1), "frac_of_peak": round(tf / MFMA_PEAK_TFLOPS, 4)}
+        del A, B, C
+        torch.cuda.empty_cache()
+    out["path"] = "torch.mm fp16 (hipBLASLt / rocBLAS), random operands, HIP events after a warm-up"
+    return out
 
 
 def configs1_leg(a, hc, dev, steps=50):
@@ -649,7 +686,10 @@ def main():
              4: "score_topk_v4_kernel (256 x 256 tiles)",
              5: "score_topk_qs_kernel (query-stationary, 128/256 queries per workgroup)",
              6: "score_topk_qw_kernel (wide query-stationary: 256 queries per workgroup in VGPRs, "
-                "full-K row stages)"}.get(st.get("score_kernel", 0), "?")
+                "full-K row stages)",
+             7: "score_topk_qw1_kernel (one wave per SIMD, 64 / 48 queries per wave in AGPR/VGPRs)",
+             8: "score_topk_qw1_kernel (8-wave form)",
+             9: "score_topk_qw1p_kernel (QW1 software-pipelined)"}.get(st.get("score_kernel", 0), "?")
     roof["kernel"] = (kname + ", fused MFMA score + top-k': sample pre-pass (v4 MAXONLY) + dense "
                       "pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
@@ -671,6 +711,13 @@ def main():
         roof["lds_dma_fill_TBps"] = round(fill / (avg_ms * 1e-3) / 1e12, 2)
 
     value = nq / (elapsed / a.steps)
+    if rank == 0 and world == 1 and not a.no_vendor_gemm and roof["bound"] == "mfma":
+        cal = vendor_gemm_leg(dev)
+        cal["this_kernel_vs_headline_shape"] = round(
+            achieved / cal["headline_shape_1024x131072x768"]["TFLOPs"], 3)
+        cal["this_kernel_vs_square"] = round(achieved / cal["square_8192"]["TFLOPs"], 3)
+        roof["vendor_gemm_calibration"] = cal
+        log(json.dumps({"vendor_gemm_calibration": cal}))
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         nr = min(a.cpu_rows, nloc)

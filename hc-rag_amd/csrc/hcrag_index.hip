@@ -64,6 +64,7 @@ struct hcr_index {
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
+  int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -416,6 +417,11 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
     case HCR_OPT_QW1_SHAPE:
       if (value < 0 || value > 3) return set_err(HCR_EINVAL, "HCR_OPT_QW1_SHAPE value %d not in [0, 3]", value);
       ix->opt_qw1_shape = value;
+      return HCR_OK;
+    case HCR_OPT_SAMPLE_STRIDE:
+      if (value != 0 && (value < 2 || value > 4096))
+        return set_err(HCR_EINVAL, "HCR_OPT_SAMPLE_STRIDE value %d not 0 or in [2, 4096]", value);
+      ix->opt_stride = value;
       return HCR_OK;
     default:
       return set_err(HCR_EINVAL, "unknown index option %d", option);
@@ -972,6 +978,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // form (every sampled row a candidate, merged; stride 512; the other tile shapes).
       const bool maxonly = !th.prepass_topk && (wide || qs || qw || qw1);
       int stride = th.sample_stride > 0 ? th.sample_stride
+                   : ix->opt_stride > 0 ? ix->opt_stride
                                         : (maxonly ? (ix->n >= kLargeCorpusRows ? kSampleStrideMaxLarge
                                                                                  : kSampleStrideMax)
                                                    : kSampleStrideDefault);

@@ -163,8 +163,12 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                software-pipelined: the previous stage's epilogue under the MFMAs).
  *   HCR_OPT_QW1_SHAPE: QW1's stage shape at D = 768 (tuning): 0 = 32-row stages, 3-deep ring,
  *                3 fragment groups in flight; 1 = 4 groups in flight; 2 = 16-row stages, 6-deep
- *                ring; 3 = both. */
-typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2 } hcr_index_option;
+ *                ring; 3 = both.
+ *   HCR_OPT_SAMPLE_STRIDE: the sampling pre-pass reads every value-th row tile (0 = the
+ *                heuristic: 64, or 128 from 4M rows; 2 .. 4096 otherwise).  A denser sample
+ *                gives a tighter seed (fewer candidate appends in the dense pass) at the cost of
+ *                a longer pre-pass. */
+typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3 } hcr_index_option;
 int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)

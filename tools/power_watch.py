@@ -50,6 +50,37 @@ for v in sys.argv[3].split(","):
 print("END", flush=True, file=sys.stderr)
 """
 
+# Vendor-GEMM ceiling under the same power cap: torch.mm (hipBLASLt / rocBLAS) on the headline's
+# GEMM shape (1024 queries x 768 . 768 x 131072-row chunks, fp16 in, fp16 out) and on a square
+# 8192^3 fp16 GEMM, each run back to back for the phase (reported as TFLOP/s in DONE lines).
+CHILD_GEMM = r"""
+import sys, time, torch
+secs = float(sys.argv[4])
+dev = torch.device("cuda", 0)
+shapes = {"g_head": (1024, 131072, 768), "g_sq": (8192, 8192, 8192), "g_head_t": (131072, 1024, 768)}
+for v in sys.argv[3].split(","):
+    M, N, K = shapes[v]
+    A = torch.randn((M, K), device=dev, dtype=torch.float16)
+    B = torch.randn((N, K), device=dev, dtype=torch.float16)
+    C = torch.empty((M, N), device=dev, dtype=torch.float16)
+    torch.mm(A, B.t(), out=C); torch.cuda.synchronize()
+    print("PHASE", v, flush=True, file=sys.stderr)
+    t0 = time.perf_counter(); n = 0
+    while time.perf_counter() - t0 < secs:
+        for _ in range(8):
+            torch.mm(A, B.t(), out=C)
+        torch.cuda.synchronize()
+        n += 8
+    dt_ = time.perf_counter() - t0
+    print("DONE", v, n, dt_, flush=True, file=sys.stderr)
+    print("TFLOPS", v, round(2.0 * M * N * K * n / dt_ / 1e12, 1), flush=True, file=sys.stderr)
+    del A, B, C
+    torch.cuda.empty_cache()
+    print("PHASE idle", flush=True, file=sys.stderr)
+    time.sleep(1.5)
+print("END", flush=True, file=sys.stderr)
+"""
+
 
 def smi_sample():
     for cmd in (["amd-smi", "metric", "--power", "--clock", "--json"],
@@ -78,10 +109,11 @@ def main():
     ap.add_argument("--shape", default="c2")
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--seconds", type=float, default=6.0)
+    ap.add_argument("--gemm", action="store_true", help="vendor GEMM phases (CHILD_GEMM)")
     a = ap.parse_args()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     log = open(os.path.join(ROOT, "gpurun_out", "power_watch.log"), "w")
-    p = subprocess.Popen([sys.executable, "-c", CHILD, ROOT, a.shape, a.variants, str(a.seconds)],
+    p = subprocess.Popen([sys.executable, "-c", CHILD_GEMM if a.gemm else CHILD, ROOT, a.shape, a.variants, str(a.seconds)],
                          stderr=subprocess.PIPE, text=True)
     os.set_blocking(p.stderr.fileno(), False)
     phase, buf, samples, done = "build", "", [], {}

@@ -19,7 +19,8 @@ import bench  # noqa: E402
 
 SHAPES = {"c2": (10_000_000, 768, "f16", 1024, 32), "c4": (12_500_000, 1024, "bf16", 8192, 64),
           "c1": (1_000_000, 384, "f16", 256, 10),
-          "c2s": (2_000_000, 768, "f16", 1024, 32), "c4s": (2_000_000, 1024, "bf16", 8192, 64)}
+          "c2s": (2_000_000, 768, "f16", 1024, 32), "c4s": (2_000_000, 1024, "bf16", 8192, 64),
+          "w8": (1_250_000, 768, "f16", 1024, 32), "w4": (2_500_000, 768, "f16", 1024, 32)}
 
 
 def main():
@@ -28,7 +29,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2",
-                    help="HCR_OPT_QW1 values, each optionally ':shape' (HCR_OPT_QW1_SHAPE)")
+                    help="HCR_OPT_QW1 values, each optionally ':shape' (HCR_OPT_QW1_SHAPE) and "
+                         "':stride' (HCR_OPT_SAMPLE_STRIDE), e.g. -1:0:32")
     a = ap.parse_args()
     import hcrag_amd as hc
     dev = torch.device("cuda", 0)
@@ -47,9 +49,10 @@ def main():
         ref = None
         for r in range(a.rounds):
             for vs in a.variants.split(","):
-                v, shape = (int(x) for x in (vs + ":0").split(":")[:2])
+                v, shape, stride = (int(x) for x in (vs + ":0:0").split(":")[:3])
                 ix.set_option(ix.OPT_QW1, v)
                 ix.set_option(ix.OPT_QW1_SHAPE, shape)
+                ix.set_option(ix.OPT_SAMPLE_STRIDE, stride)
                 ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
                 torch.cuda.synchronize()
                 ix.set_timing(True)
@@ -69,17 +72,19 @@ def main():
                 fl = 2.0 * B * N * D
                 rec = {"shape": sh, "variant": vs, "round": r, "score_kernel": st["score_kernel"],
                        "score_ms": round(min(kms), 4), "score_ms_med": round(sorted(kms)[len(kms) // 2], 4),
-                       "wall_ms": round(min(walls), 4), "mfma_frac": round(fl / (min(kms) * 1e-3) / 2.5e15, 4),
+                       "wall_ms": round(min(walls), 4), "wall_ms_med": round(sorted(walls)[len(walls) // 2], 4), "mfma_frac": round(fl / (min(kms) * 1e-3) / 2.5e15, 4),
                        "wg": st["workgroups"], "P": st["partitions"], "unit": st["unit_kernel"], "widened": st["widened_queries"],
                        "fallback": st["fallback_queries"], "ids_equal_first": same}
                 print(json.dumps(rec), flush=True)
-                summary.setdefault((sh, vs), []).append(min(kms))
+                summary.setdefault((sh, vs), []).append((min(kms), min(walls)))
         ix.close()
         del Q, S, I
         torch.cuda.empty_cache()
     for (sh, v), xs in summary.items():
-        print(json.dumps({"summary": sh, "variant": v, "score_ms_min": round(min(xs), 4),
-                          "score_ms_med": round(sorted(xs)[len(xs) // 2], 4)}), flush=True)
+        ks, ws = sorted(x[0] for x in xs), sorted(x[1] for x in xs)
+        print(json.dumps({"summary": sh, "variant": v, "score_ms_min": round(ks[0], 4),
+                          "score_ms_med": round(ks[len(ks) // 2], 4), "wall_ms_min": round(ws[0], 4),
+                          "wall_ms_med": round(ws[len(ws) // 2], 4)}), flush=True)
 
 
 if __name__ == "__main__":
