@@ -65,6 +65,7 @@ struct hcr_index {
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
+  int opt_qs = 0;               // HCR_OPT_QS_FORM (0: the heuristic)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -423,6 +424,10 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
         return set_err(HCR_EINVAL, "HCR_OPT_SAMPLE_STRIDE value %d not 0 or in [2, 4096]", value);
       ix->opt_stride = value;
       return HCR_OK;
+    case HCR_OPT_QS_FORM:
+      if (value < 0 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not in [0, 2]", value);
+      ix->opt_qs = value;
+      return HCR_OK;
     default:
       return set_err(HCR_EINVAL, "unknown index option %d", option);
   }
@@ -518,11 +523,12 @@ static const TestHooks& hooks() {
 
 // qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h); qw1: the
 // one-wave-per-SIMD form (score_qw1.h), spread = its DMA issue spread over the MFMA groups
-struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false, nw8 = false, pipe = false; };
+struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false, nw8 = false, pipe = false,
+               qs4 = false; };
 // qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
 // QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1,
-                    int qw1_shape = 0) {
+                    int qw1_shape = 0, int opt_qs = 0) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
@@ -548,6 +554,14 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
   // vs 4.45, B = 256 4.52 vs 4.59; 1M x 384 B = 32 0.187 vs 0.295, B = 256 0.290 vs 0.331.
   if (nq <= hooks().qs_max) {
+    // QS4: 128-query 4-wave workgroups, two per CU (score_qs.h).  The default for 129-256
+    // queries (KS <= 12: configs[1]); HCR_OPT_QS_FORM = 2 also from 65, 1 never.  r03 A/B at
+    // 1M x 384, B = 256 (score ms): 0.2688 vs 0.2702 at stride 64, 0.2637 vs 0.2701 at 32.
+    if (opt_qs != 1 && nq > (opt_qs == 2 ? 64 : 128) && qs_supported(ld, 2)) {
+      V3Cfg c{128, 128, 4, true};
+      c.qs4 = true;
+      return c;
+    }
     // 129-256 queries with KS <= 12: one 256-query block on 128-row tiles (each row filled
     // into LDS once instead of once per 128-query block)
     if (nq > 128 && qs_supported(ld, 2)) return {128, 256, 8, true};
@@ -606,7 +620,7 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
            ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr, ix->w_qhat.p, a.nqb, a.P,
            a.nvt, a.tstride, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
-           c.qt == 256 ? 2 : 1};
+           (c.qt == 256 || c.qs4) ? 2 : 1, c.qs4 ? 4 : 8};
   return launch_qs(ix->dtype, q, st);
 }
 
@@ -746,12 +760,20 @@ static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, i
 static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile in 512
                                                   // (estimated seed, r01d sweep at 10M x 768,
                                                   // B = 1024: 64 -> 512 saves ~0.5 ms)
-static constexpr int kSampleStrideMax = 64;      // ... of the MAXONLY pre-pass (r01d), and
-static constexpr int kSampleStrideMaxLarge = 128; // from kLargeCorpusRows rows: the seed's global
-static constexpr int64_t kLargeCorpusRows = 4000000;  // rank ~1000 instead of ~600 is a smaller
-                                                  // fraction of a large corpus (r02: 10M x 768
-                                                  // B = 1024 -0.13 ms per search with 128; 1M x
-                                                  // 384 B = 256 +0.016 ms: 64 there)
+// MAXONLY pre-pass stride: the largest power of two in [16, 128] that keeps >= 150 row tiles
+// (~38k rows) in the sample.  The seed's global rank is ~j / (sampled fraction) (j = 8-25, see
+// search_pass): a small corpus needs a denser sample for a seed tight enough to keep the dense
+// pass's appends rare, a large one reaches it at 128.  r03 A/B (tools/r03_seed.sh, score ms):
+// 1M x 384 B = 256 stride 64 0.270 / 32 0.264 / 16 0.260 (QS4); 1.25M x 768 B = 1024 (the W = 8
+// rank shape) 64 1.746 / 32 1.712 / 16 1.723 / 8 1.873; 2.5M x 768 64 3.427 / 32 3.431 / 16
+// 3.635; 10M x 768 128 13.20 / 64 13.23 / 32 13.48.
+static constexpr int kSampleMinTiles = 150;
+static constexpr int kSampleStrideMin = 16, kSampleStrideMaxAll = 128;
+static int maxonly_stride(int64_t ntiles) {
+  int s = kSampleStrideMin;
+  while (s * 2 <= kSampleStrideMaxAll && ntiles / (s * 2) >= kSampleMinTiles) s *= 2;
+  return s;
+}
 static constexpr int kPrepassMinTilesPerWg = 4;   // ... when each dense workgroup has >= 4 tiles
                                                   // (r01g, configs[1] 1M x 384 B = 256: 15 tiles
                                                   // per workgroup; seeded 0.32 ms vs cold 1.84 ms)
@@ -890,7 +912,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
                           qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
-                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qw1_shape);
+                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qw1_shape, ix->opt_qs);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   if (hooks().debug_cfg)
     fprintf(stderr, "[hcrag] search_pass nq=%d n=%lld ld=%d kp=%d unit_dev=%.3g rho=%.3g mask=%d "
@@ -906,7 +928,8 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
   const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : qw1 ? qw1_cap(kp, ix->ld) : next_pow2(kp + tr);
-  const int wg_target = ver == 1 ? 512 : 256;
+  // (QS4: two 4-wave workgroups per CU)
+  const int wg_target = (ver == 1 || (ver == 3 && c3.qs4)) ? 512 : 256;
   // (QW: one workgroup per CU -- its LDS -- so at most 256 workgroups: one round)
   int P = qw1 ? qw1_partitions(nqb, ntiles)
                : qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
@@ -944,7 +967,8 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
   if (ix->stats.score_kernel == 0)
-    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? (c3.pipe ? 9 : c3.nw8 ? 8 : 7) : qw ? 6 : qs ? 5 : wide ? 4 : 3;
+    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? (c3.pipe ? 9 : c3.nw8 ? 8 : 7) : qw ? 6
+                           : qs ? (c3.qs4 ? 10 : 5) : wide ? 4 : 3;
 
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)
@@ -979,8 +1003,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       const bool maxonly = !th.prepass_topk && (wide || qs || qw || qw1);
       int stride = th.sample_stride > 0 ? th.sample_stride
                    : ix->opt_stride > 0 ? ix->opt_stride
-                                        : (maxonly ? (ix->n >= kLargeCorpusRows ? kSampleStrideMaxLarge
-                                                                                 : kSampleStrideMax)
+                                        : (maxonly ? maxonly_stride((ix->n + 255) / 256)
                                                    : kSampleStrideDefault);
       constexpr int kMaxUnits = 4096;
       // MAXONLY runs on the 256 x 256 kernel: nqpad / 256 query blocks, 256-row tiles (the

@@ -98,9 +98,9 @@ __device__ __forceinline__ void qs_read_u32x8(uint32_t a, uint32_t (&w)[8]) {
   w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
-template <int NST, int KS, int RT_, int NQ>
+template <int NST, int KS, int RT_, int NQ, int NW = 8>
 struct QsLayout {
-  static constexpr int RT = RT_, QT = 128 * NQ;
+  static constexpr int RT = RT_, QT = 16 * NQ * NW;
   static constexpr int SPT = KS / 2;                       // stages per tile (64-deep stages)
   static constexpr int STAGE = RT * 128;                   // RT rows x 64 k: two 32-deep halves
   // tile slots of inverse norms / bounds / mask words: a tile's slot must outlive the NST-1
@@ -123,20 +123,29 @@ struct QsLayout {
 // NQ x 16 queries per wave on RT-row tiles: (1, 256) -- 128 queries per workgroup, any
 // KS <= 24 -- or (2, 128) -- 256 queries per workgroup for KS <= 12 (2 x KS x 4 VGPRs of query
 // fragments): every row is filled into LDS once per 256 queries instead of once per 128.
+//
+// NW = 4 ("QS4"): 4 waves (one per SIMD) and a 4 x 16 KiB ring -- ~68 KiB of LDS, so two
+// workgroups share a CU, each with its own barrier: the 8-wave form keeps every wave of the CU
+// in lock step (one barrier per stage, every wave's tile epilogue at the same time: the MFMA
+// pipe idles through epilogues and barrier skew, ~half of each tile at configs[1]); two
+// independent 4-wave workgroups drift apart, so one's epilogue runs under the other's MFMAs.
+// Rows are then filled into LDS once per 128 queries (the second query block's workgroup
+// reads them from the XCD's L2: consecutive workgroups of one XCD).
 template <typename TM, int CAP, int KS, bool UNIT, int NQ = 1, int RT_ = 256,
-          int NST = (RT_ == 256 ? 4 : 8)>
-__global__ void __launch_bounds__(V3_NT, 1)
+          int NST = (RT_ == 256 ? 4 : 8), int NW = 8>
+__global__ void __launch_bounds__(NW * 64, 8 / NW)
 score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = QsLayout<NST, KS, RT_, NQ>;
+  using L = QsLayout<NST, KS, RT_, NQ, NW>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int RT = L::RT, QT = L::QT, MT = RT / 16, D = NST - 1, SPT = L::SPT;
   constexpr int PPH = RT / 16;            // 1 KiB LDS-DMA pieces per 32-deep half of a stage
-  constexpr int PPW = 2 * PPH / 8;        // ... per wave per stage
+  constexpr int PPW = 2 * PPH / NW;       // ... per wave per stage
+  static_assert((2 * PPH) % NW == 0, "stage pieces per wave");
   constexpr int NG = MT / 2;              // groups of 4 row blocks per stage (2 halves)
   static_assert(CAP >= 2 * RT, "candidate buffer must hold a tile's appends after a compaction");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
@@ -188,12 +197,13 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       uniform_ptr(tau_g + qbase), (short)0, QT * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t msk_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(mask), (short)0, 0x7FFFFFFF, 0x00020000);
-  // tile-start pieces: inverse norms (not read by the UNIT kernel), bounds, mask words
-  const bool extra = (!UNIT && wave == 7) || wave == 6 || (wave == 5 && mask);
+  // tile-start pieces: inverse norms (not read by the UNIT kernel), bounds, mask words -- by
+  // the last three waves
+  const bool extra = (!UNIT && wave == NW - 1) || wave == NW - 2 || (wave == NW - 3 && mask);
 
   const int nsteps = (t1 - t0) * SPT;
   // Issue virtual tile vt's stage SP2 into ring slot `slot`.  Every wave issues its PPW row
-  // pieces; at a tile's first stage waves 7 / 6 / 5 also issue the tile's inverse norms, query
+  // pieces; at a tile's first stage waves NW-1 / NW-2 / NW-3 also issue the tile's inverse norms, query
   // bounds and mask words (SP2 is a compile-time constant, so is that choice).  The per-lane
   // offsets are re-derived from `lane` here rather than kept live across the loop.
   auto issue_stage = [&](auto sp2_c, int vt_, int slot_) __attribute__((always_inline)) {
@@ -206,18 +216,18 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         uniform_ptr(rows_b + (size_t)tile * RT * ldb), (short)0, RT * ldb, 0x00020000);
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int j = wave + 8 * i;            // piece: half j / PPH, rows (j % PPH) * 16 ..
+      const int j = wave + NW * i;           // piece: half j / PPH, rows (j % PPH) * 16 ..
       dma16(a_rsrc, sa + j * 1024, voff, (j % PPH) * 16 * ldb + (2 * SP2 + j / PPH) * (V3_BK * 2));
     }
     if constexpr (SP2 == 0) {
       const int is = vt % L::NIS;
       int l16;
       asm volatile("v_lshlrev_b32 %0, 4, %1" : "=v"(l16) : "v"(lane));
-      if (!UNIT && wave == 7 && lane < RT / 4)   // RT inverse norms
+      if (!UNIT && wave == NW - 1 && lane < RT / 4)   // RT inverse norms
         dma16(inv_rsrc, lds + L::INV + is * L::INV_SLOT, l16, tile * (RT * 4));
-      if (wave == 6 && lane < QT / 4)
+      if (wave == NW - 2 && lane < QT / 4)
         dma16(tg_rsrc, lds + L::TG + is * L::TG_SLOT, l16, 0);
-      if (wave == 5 && mask && lane < RT / 32)
+      if (wave == NW - 3 && mask && lane < RT / 32)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             msk_rsrc, (__attribute__((address_space(3))) void*)(lds + L::MSK + is * 64),
             4, l16 >> 2, tile * (RT / 8), 0, 0);
@@ -235,6 +245,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   floatx4 acc[MT][NQ];
 #ifdef HCR_QS_STAMPS
   unsigned long long st_wait = 0, st_comp = 0, st_epi = 0, st_fast = 0, st_slow_n = 0, st_t0, st_t1, st_t2;
+  // the in-kernel clock: s_memtime (shader clock) over s_memrealtime (100 MHz) across the loop
+  unsigned long long st_c0, st_r0, st_c1, st_r1;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_c0), "=s"(st_r0)::"memory");
 #endif
   bool need = false;                           // some query's buffer must be compacted
   // the lane's query's local k'-th key (only this wave changes it: kept in registers) and its
@@ -483,9 +496,11 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
   }
 #ifdef HCR_QS_STAMPS
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_c1), "=s"(st_r1)::"memory");
   if (lane == 0 && b < 4096) {
     unsigned long long* o = hcr_qs_stamps + ((size_t)b * 8 + wave) * 8;
     o[0] = st_wait; o[1] = st_comp; o[2] = st_epi; o[3] = (unsigned long long)(t1 - t0);
+    o[6] = st_c1 - st_c0; o[7] = st_r1 - st_r0;
     o[4] = st_fast; o[5] = st_slow_n;
   }
 #endif

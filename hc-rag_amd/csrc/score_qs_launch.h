@@ -20,10 +20,13 @@ struct QsArgs {
   bool unit;                 // raw dot products as coarse scores (L2-normalised corpus)
   int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles);
                              // QW1: its tuning shape (HCR_OPT_QW1_SHAPE)
+  int nw = 8;                // QS waves per workgroup: 8, or 4 with nq_blocks 2 (QS4: two
+                             // 128-query workgroups per CU)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128
-// queries per workgroup on 256-row tiles; 2: 256 queries on 128-row tiles).
+// queries per workgroup on 256-row tiles; 2: 256 queries on 128-row tiles, or 128 per 4-wave
+// workgroup in the QS4 form).
 bool qs_supported(int ld, int nq_blocks);
 // Candidate buffer slots per query for k'.
 int qs_cap(int kp);

@@ -200,11 +200,17 @@ def _check_top_k(k: int) -> int:
 # the GPU vector half: an id-keyed set of rows on one hcr_index
 # ---------------------------------------------------------------------------------------------
 class _GpuRows:
-    """Node embeddings on the MI355X index, keyed by node id (tombstoned deletes; metadata kept
-    host-side for the equality filters)."""
+    """Node embeddings on the MI355X index, keyed by node id (metadata kept host-side for the
+    equality filters).  Deletes and replacements tombstone a row (masked out of every search);
+    once tombstones reach COMPACT_MIN rows and COMPACT_FRAC of the index, the live rows are
+    re-ingested into a fresh index and the old one's HBM is freed (``compact``)."""
+
+    COMPACT_MIN = 1024
+    COMPACT_FRAC = 0.25
 
     def __init__(self, dim: int, dtype: str, device: int):
         self.dim = int(dim)
+        self.dtype, self.device = dtype, device
         self.index = VectorIndex(dim, dtype=dtype, device=device)
         # fp32 rows are stored as given (exact sklearn / llama-index cosine of the node
         # embeddings); 16-bit rows are L2-normalised in fp64 before rounding
@@ -235,6 +241,7 @@ class _GpuRows:
             self.nodes.append(n)
             out.append(nid)
         self.deleted = np.concatenate([self.deleted, np.zeros(len(nodes), dtype=bool)])
+        self._maybe_compact()
         return out
 
     def delete(self, pred) -> None:
@@ -243,6 +250,28 @@ class _GpuRows:
                 self.deleted[r] = True
                 if self.row_of.get(nid) == r:
                     del self.row_of[nid]
+        self._maybe_compact()
+
+    def _maybe_compact(self) -> None:
+        nd = int(self.deleted.sum())
+        if nd >= self.COMPACT_MIN and nd >= self.COMPACT_FRAC * len(self.ids):
+            self.compact()
+
+    def compact(self) -> None:
+        """Re-ingest the live rows (their nodes' embeddings, in insertion order, so ties still
+        break by insertion order) into a fresh index; the tombstoned rows' HBM is released."""
+        live = np.flatnonzero(~self.deleted)
+        fresh = VectorIndex(self.dim, dtype=self.dtype, device=self.device)
+        if live.size:
+            E = np.asarray([_node_embedding(self.nodes[r]) for r in live], dtype=np.float32)
+            fresh.add(E, normalize=self.normalize)
+        old, self.index = self.index, fresh
+        old.close()
+        self.ids = [self.ids[r] for r in live]
+        self.meta = [self.meta[r] for r in live]
+        self.nodes = [self.nodes[r] for r in live]
+        self.row_of = {nid: j for j, nid in enumerate(self.ids)}
+        self.deleted = np.zeros(len(self.ids), dtype=bool)
 
     def mask(self, query) -> Optional[np.ndarray]:
         pairs = _filter_pairs(getattr(query, "filters", None))

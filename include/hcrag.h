@@ -148,7 +148,8 @@ typedef struct {
                                  (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW,
                                  7 QW1 (one wave per SIMD, 64 / 48 queries per wave),
                                  8 QW1 in its 8-wave form (D = 384: two row halves per query set),
-                                 9 QW1P (QW1 software-pipelined, HCR_OPT_QW1 = 5) */
+                                 9 QW1P (QW1 software-pipelined, HCR_OPT_QW1 = 5),
+                                 10 QS4 (two 4-wave query-stationary workgroups per CU) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
@@ -165,10 +166,16 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                3 fragment groups in flight; 1 = 4 groups in flight; 2 = 16-row stages, 6-deep
  *                ring; 3 = both.
  *   HCR_OPT_SAMPLE_STRIDE: the sampling pre-pass reads every value-th row tile (0 = the
- *                heuristic: 64, or 128 from 4M rows; 2 .. 4096 otherwise).  A denser sample
+ *                heuristic: the largest power of two in [16, 128] leaving >= 150 sampled 256-row
+ *                tiles; 2 .. 4096 otherwise).  A denser sample
  *                gives a tighter seed (fewer candidate appends in the dense pass) at the cost of
- *                a longer pre-pass. */
-typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3 } hcr_index_option;
+ *                a longer pre-pass.
+ *   HCR_OPT_QS_FORM: the query-stationary kernel's form for 65-256 queries at D <= 384: 0 = the
+ *                heuristic (QS4 from 129 queries), 1 = never QS4 (one 8-wave workgroup per CU:
+ *                256 queries on 128-row tiles from 129 queries), 2 = QS4 from 65 queries
+ *                (128-query 4-wave workgroups, two per CU). */
+typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3,
+               HCR_OPT_QS_FORM = 4 } hcr_index_option;
 int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)

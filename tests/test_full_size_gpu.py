@@ -80,7 +80,7 @@ def test_configs1_full_size(env):
     """configs[1]: 1,000,000 x 384 f16, 256 queries, top-10 (its default score kernel)."""
     B = 256
     st = _run(env, 1_000_000, 384, B, 10, 2000, np.r_[0:8, B // 2:B // 2 + 8, B - 8:B])
-    assert st["score_kernel"] in (5, 6, 7), st
+    assert st["score_kernel"] in (5, 6, 7, 10), st
 
 
 def test_configs2_full_size(env):

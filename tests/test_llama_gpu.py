@@ -92,3 +92,29 @@ def test_vector_store_large_top_k_and_replace():
     assert "n5" not in res.ids[1:]
     with pytest.raises(ValueError):
         vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=5000))
+
+
+def test_vector_store_deletes_compact_hbm():
+    """Tombstoned deletes are compacted away (llama_compat._GpuRows.compact): past COMPACT_MIN
+    tombstones the live rows are re-ingested into a fresh index, insertion order kept, and the
+    answers stay those of the oracle over the live rows (ids, fp64 scores, tie order)."""
+    from hcrag_amd.llama_compat import MI355XVectorStore, TextNodeLite, VectorStoreQuery
+    rng = np.random.default_rng(7)
+    n, D = 3000, 64
+    E = rng.standard_normal((n, D))
+    E[2001] = E[17]                                       # a tie across the compaction
+    vs = MI355XVectorStore(D, dtype="f32")
+    vs.add([TextNodeLite(id_=f"n{i}", embedding=E[i].tolist(), metadata={"ref_doc_id": f"d{i // 2}"})
+            for i in range(n)])
+    gone = set(range(40, 1640))                           # docs d20 .. d819: 1600 rows
+    for d in range(20, 820):
+        vs.delete(f"d{d}")
+    live = np.array([i for i in range(n) if i not in gone])
+    assert len(vs.client) < n                             # compacted at 1024 tombstones
+    assert len(vs.client) == n - 1024
+    q = E[17] + 0.01 * rng.standard_normal(D)
+    res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=50))
+    es, ei = O.cosine_topk(q[None].astype(np.float32), E[live].astype(np.float32), 50)
+    assert res.ids == [f"n{live[j]}" for j in ei[0]]
+    np.testing.assert_allclose(res.similarities, es[0], rtol=0, atol=1e-12)
+    assert res.ids[:2] == ["n17", "n2001"]

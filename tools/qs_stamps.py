@@ -1,6 +1,6 @@
 """Where the QS score kernel's time goes, from the stamps build (Makefile target `stamps`).
 
-    HCRAG_LIB=hc-rag_amd/lib/stamps/libhcrag_hip.so python tools/qs_stamps.py ROWS DIM BATCH
+    HCRAG_LIB=hc-rag_amd/lib/stamps/libhcrag_hip.so python tools/qs_stamps.py ROWS DIM BATCH [QS_FORM [STRIDE]]
 
 Runs a few searches, then reads the per-wave s_memtime sums of the last launch: stage wait
 (vmcnt + barrier), stage issue (DMA + fragment reads + MFMAs), tile epilogue; prints them per
@@ -17,6 +17,8 @@ import hcrag_amd  # noqa: E402
 from hcrag_amd import _lib  # noqa: E402
 
 N, D, B = (int(x) for x in sys.argv[1:4])
+QSF = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+STRIDE = int(sys.argv[5]) if len(sys.argv) > 5 else 0
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 ix = hcrag_amd.VectorIndex(D, "f16", device=0)
@@ -27,9 +29,12 @@ for a in range(0, N, chunk):
     torch.cuda.synchronize()
     ix.add_device(xs.data_ptr(), b - a, _lib.HCR_F32, normalize=True)
 torch.cuda.synchronize()
+ix.set_option(ix.OPT_QS_FORM, QSF)
+ix.set_option(ix.OPT_SAMPLE_STRIDE, STRIDE)
 Q = np.random.default_rng(1).standard_normal((B, D)).astype(np.float32)
-for _ in range(3):
+for _ in range(20):        # back to back: the clock settles under load
     ix.search(Q, 10)
+print("score_kernel", ix.last_stats()["score_kernel"])
 lib = _lib.lib()
 fn = lib.hcr_debug_qs_stamps
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
@@ -48,7 +53,11 @@ print(f"epilogue split: max/test part {f.sum() / tiles:.1f} per tile; slow path 
       f"{sn.sum() / tiles:.3f} of the tiles, {(e.sum() - f.sum()) / max(sn.sum(), 1):.1f} ticks per entry")
 tot = w.sum() + c.sum() + e.sum()
 print(f"shares: wait {w.sum() / tot:.3f}  issue {c.sum() / tot:.3f}  epilogue {e.sum() / tot:.3f}")
+clk, rt = a[:, :, 6][live], a[:, :, 7][live]
+print(f"in-kernel clock over the tile loop: {np.median(clk / np.maximum(rt, 1)) * 100:.0f} MHz (median over waves)")
 for wv in range(8):
     m = a[:, wv, 3] > 0
+    if not m.any():
+        continue
     print(f"  wave {wv}: wait {a[m, wv, 0].sum() / a[m, wv, 3].sum():.1f} issue {a[m, wv, 1].sum() / a[m, wv, 3].sum():.1f} "
           f"epi {a[m, wv, 2].sum() / a[m, wv, 3].sum():.1f}")

@@ -49,10 +49,11 @@ def main():
         ref = None
         for r in range(a.rounds):
             for vs in a.variants.split(","):
-                v, shape, stride = (int(x) for x in (vs + ":0:0").split(":")[:3])
+                v, shape, stride, qsf = (int(x) for x in (vs + ":0:0:0").split(":")[:4])
                 ix.set_option(ix.OPT_QW1, v)
                 ix.set_option(ix.OPT_QW1_SHAPE, shape)
                 ix.set_option(ix.OPT_SAMPLE_STRIDE, stride)
+                ix.set_option(ix.OPT_QS_FORM, qsf)
                 ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
                 torch.cuda.synchronize()
                 ix.set_timing(True)
