@@ -120,6 +120,74 @@ __device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E], int lane) {
   bitonic_all_desc<E, 1, 6 + LOGE>(v, lane);
 }
 
+// ---- (hi, lo) pairs, lexicographic, descending: the same network as wave_sort_desc ----
+template <int E, int LOGSIZE>
+__device__ __forceinline__ void bitonic_stage_desc_pair(uint64_t (&h)[E], uint64_t (&l)[E], int lane) {
+  constexpr int size = 1 << LOGSIZE;
+#pragma unroll
+  for (int ld2 = LOGSIZE - 1; ld2 >= 0; --ld2) {
+    const int d = 1 << ld2;
+    if (d >= E) {
+      const int lm = d / E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        const uint64_t oh = shfl_xor_u64(h[e], lm), ol = shfl_xor_u64(l[e], lm);
+        const bool lower = (i & d) == 0;
+        const bool desc = (i & size) == 0;
+        const bool gt = h[e] > oh || (h[e] == oh && l[e] > ol);   // mine is the larger
+        const bool take_mine = (lower == desc) ? gt : !gt;
+        if (!take_mine) { h[e] = oh; l[e] = ol; }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if ((e & d) == 0) {
+          const int e2 = e | d;
+          const int i = lane * E + e;
+          const bool desc = (i & size) == 0;
+          const bool gt = h[e] > h[e2] || (h[e] == h[e2] && l[e] > l[e2]);
+          if (gt != desc) {
+            const uint64_t th = h[e], tl = l[e];
+            h[e] = h[e2]; l[e] = l[e2]; h[e2] = th; l[e2] = tl;
+          }
+        }
+      }
+    }
+  }
+}
+template <int E, int LOGSIZE, int LOGN>
+__device__ __forceinline__ void bitonic_all_desc_pair(uint64_t (&h)[E], uint64_t (&l)[E], int lane) {
+  if constexpr (LOGSIZE <= LOGN) {
+    bitonic_stage_desc_pair<E, LOGSIZE>(h, l, lane);
+    bitonic_all_desc_pair<E, LOGSIZE + 1, LOGN>(h, l, lane);
+  }
+}
+
+// Wave 0 sorts a[0, 64 E) (LDS) in registers; the caller synchronises before and after.
+template <int E>
+__device__ __forceinline__ void wave0_sort_lds_u64(uint64_t* a) {
+  const int lane = threadIdx.x;
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = a[lane * E + e];
+  wave_sort_desc<E>(v, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) a[lane * E + e] = v[e];
+}
+template <int E>
+__device__ __forceinline__ void wave0_sort_lds_pair(uint64_t* hi, uint64_t* lo) {
+  constexpr int LOGE = (E == 1) ? 0 : (E == 2) ? 1 : (E == 4) ? 2 : 3;
+  static_assert((1 << LOGE) == E, "E must be a power of two <= 8");
+  const int lane = threadIdx.x;
+  uint64_t h[E], l[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { h[e] = hi[lane * E + e]; l[e] = lo[lane * E + e]; }
+  bitonic_all_desc_pair<E, 1, 6 + LOGE>(h, l, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) { hi[lane * E + e] = h[e]; lo[lane * E + e] = l[e]; }
+}
+
 // ---- block-wide bitonic sort in LDS, descending, M a power of two ---------------------
 __device__ __forceinline__ void block_sort_desc_u64(uint64_t* a, int M) {
   for (int size = 2; size <= M; size <<= 1) {
@@ -135,6 +203,20 @@ __device__ __forceinline__ void block_sort_desc_u64(uint64_t* a, int M) {
     }
   }
 }
+// M in {64, 128, 256, 512} (a power of two): one wave sorts in registers -- two block barriers
+// instead of the network's log2(M) (log2(M) + 1) / 2 (21 at M = 64); larger M: the block network.
+// Called by every thread of the block, after the keys are in LDS and visible (synchronised).
+__device__ __forceinline__ void block_sort_desc_u64_fast(uint64_t* a, int M) {
+  if (M > 512 || M < 64) { block_sort_desc_u64(a, M); return; }
+  if (threadIdx.x < 64) {
+    if (M == 64) wave0_sort_lds_u64<1>(a);
+    else if (M == 128) wave0_sort_lds_u64<2>(a);
+    else if (M == 256) wave0_sort_lds_u64<4>(a);
+    else wave0_sort_lds_u64<8>(a);
+  }
+  __syncthreads();
+}
+
 // Pairs (hi, lo) compared lexicographically, descending.
 __device__ __forceinline__ void block_sort_desc_pair(uint64_t* hi, uint64_t* lo, int M) {
   for (int size = 2; size <= M; size <<= 1) {
@@ -151,6 +233,16 @@ __device__ __forceinline__ void block_sort_desc_pair(uint64_t* hi, uint64_t* lo,
       __syncthreads();
     }
   }
+}
+__device__ __forceinline__ void block_sort_desc_pair_fast(uint64_t* hi, uint64_t* lo, int M) {
+  if (M > 512 || M < 64) { block_sort_desc_pair(hi, lo, M); return; }
+  if (threadIdx.x < 64) {
+    if (M == 64) wave0_sort_lds_pair<1>(hi, lo);
+    else if (M == 128) wave0_sort_lds_pair<2>(hi, lo);
+    else if (M == 256) wave0_sort_lds_pair<4>(hi, lo);
+    else wave0_sort_lds_pair<8>(hi, lo);
+  }
+  __syncthreads();
 }
 
 }  // namespace hcr

@@ -512,62 +512,63 @@ attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ 
 
 // Reference-precision attention for short sequences (S <= 64, the query-embedding regime) on
 // the f32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation; MICROARCH
-// "FP32-input MFMA"): one 64-thread workgroup per (sequence, head); Q, K, V staged in LDS
-// (rows padded to DH + 1 floats: conflict-free column reads); S = Q·Kᵀ / sqrt(DH) + key mask
-// as NT x NT 16x16 tiles, the row softmax across the 16 lanes of a tile row, P through LDS,
-// O = P·V as NT x DH/16 tiles scaled by 1 / row sum.  r02 profile, bge-base S = 32: the
-// wave-per-query kernel (attention_f32_kernel) took 399 us per layer call.
+// "FP32-input MFMA"): one 64-thread workgroup per (sequence, head).  Q, K and V go from global
+// memory straight into the lanes' MFMA operand registers as 16-byte loads, with no LDS staging:
+//  * Q.K^T sums over d in any order, so lane (lr, lk) holds the float4 chunks lk + 4u (u < DH/16)
+//    of rows t*16 + lr of Q and of K, and k-step 4u + w of the MFMA takes element w of chunk u:
+//    the 4 k-values of a step are d = 16u + 4lk + w (lk = 0..3), every d once over the DH/4 steps;
+//  * O = P.V: lane (lr, lk) computes columns 4 lr + dt (dt < 4) of a 16-column block set, so its
+//    V operand at step j is the float4 V[4j + lk][4 lr .. 4 lr + 3];
+// only P goes through LDS (the softmax's C layout -> the A layout of P.V).  S = Q.K^T / sqrt(DH)
+// + key mask as NT x NT 16x16 tiles, the row softmax across the 16 lanes of a tile row, O = P.V
+// scaled by 1 / row sum.  LDS per workgroup 29 -> 4.4 KiB at bge-base S = 32 (r02: Q, K, V staged
+// in LDS, 124 us per layer call, latency-bound at 5 workgroups per CU; r03 with 4-byte operand
+// loads from global, 192 us: 16-line gathers; the wave-per-query attention_f32_kernel: 399 us).
 __host__ __device__ inline size_t attention_f32_mfma_lds(int nt, int dh) {
   const int s16 = 16 * nt;
-  return ((size_t)3 * s16 * (dh + 1) + (size_t)s16 * (s16 + 1) + s16) * 4;
+  (void)dh;
+  return ((size_t)s16 * (s16 + 1) + s16) * 4;
 }
 template <int DH, int NT>
 __global__ void __launch_bounds__(64)
 attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
                           int H, int heads, _Float16* __restrict__ ctx) {
-  constexpr int S16 = 16 * NT, LD = DH + 1, LP = S16 + 1;
+  constexpr int S16 = 16 * NT, LP = S16 + 1, CU = DH / 16, JI = S16 / 4;
+  static_assert(DH % 16 == 0 && DH / 4 <= 16 * 4, "head size");
   extern __shared__ __attribute__((aligned(16))) float attm_sm[];
-  float* Qs = attm_sm;
-  float* Ks = Qs + S16 * LD;
-  float* Vs = Ks + S16 * LD;
-  float* Ps = Vs + S16 * LD;
+  float* Ps = attm_sm;
   float* mk = Ps + S16 * LP;
   const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
   const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
   const size_t row0 = (size_t)bidx * S;
   const int ld3 = 3 * H;
-  // stage Q, K, V (rows >= S zero): a batch of up to 8 float4 of each per lane loaded before any
-  // is written to LDS (one memory latency per batch; load-store pairs one at a time cost one
-  // latency each: r02, 147 us per layer call at bge-base S = 32)
-  constexpr int IT = S16 * (DH / 4) / 64;
-  constexpr int BT = IT <= 8 ? IT : IT % 8 == 0 ? 8 : IT % 6 == 0 ? 6 : 4;
-  static_assert(IT % BT == 0, "staging batches");
+  const float* base = qkv + row0 * ld3 + (size_t)h * DH;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // operands (rows >= S are zero: their P entries are 0, and 0 x V must not meet a NaN)
+  float4 qa[NT][CU], kb[NT][CU];
 #pragma unroll
-  for (int b0 = 0; b0 < IT; b0 += BT) {
-    float4 q[BT], k[BT], v[BT];
+  for (int t = 0; t < NT; ++t) {
+    const int r = t * 16 + lr;
+    const float4* p = reinterpret_cast<const float4*>(base + (size_t)(r < S ? r : 0) * ld3) + lk;
 #pragma unroll
-    for (int u = 0; u < BT; ++u) {
-      const int e = lane + 64 * (b0 + u);
-      const int j = e / (DH / 4), d = (e % (DH / 4)) * 4;
-      q[u] = k[u] = v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j < S) {
-        const float* base = qkv + (row0 + j) * ld3 + h * DH + d;
-        q[u] = *reinterpret_cast<const float4*>(base);
-        k[u] = *reinterpret_cast<const float4*>(base + H);
-        v[u] = *reinterpret_cast<const float4*>(base + 2 * H);
-      }
+    for (int u = 0; u < CU; ++u) {            // (row clamped above: the loads stay in bounds)
+      qa[t][u] = p[4 * u];
+      kb[t][u] = p[H / 4 + 4 * u];
     }
+    if (r >= S) {
 #pragma unroll
-    for (int u = 0; u < BT; ++u) {
-      const int e = lane + 64 * (b0 + u);
-      const int j = e / (DH / 4), d = (e % (DH / 4)) * 4;
-      float* qd = Qs + j * LD + d;
-      float* kd = Ks + j * LD + d;
-      float* vd = Vs + j * LD + d;
-      qd[0] = q[u].x; qd[1] = q[u].y; qd[2] = q[u].z; qd[3] = q[u].w;
-      kd[0] = k[u].x; kd[1] = k[u].y; kd[2] = k[u].z; kd[3] = k[u].w;
-      vd[0] = v[u].x; vd[1] = v[u].y; vd[2] = v[u].z; vd[3] = v[u].w;
+      for (int u = 0; u < CU; ++u) { qa[t][u] = z4; kb[t][u] = z4; }
     }
+  }
+  // (DH / 16 column groups of 4: lane lr's columns 4 lr + dt only exist for lr < DH / 4)
+  constexpr int VL = DH / 4;
+  float4 vb[JI];
+#pragma unroll
+  for (int j = 0; j < JI; ++j) {
+    const int r = 4 * j + lk;
+    const bool ok = r < S && lr < VL;
+    vb[j] = *(reinterpret_cast<const float4*>(base + (size_t)(ok ? r : 0) * ld3 + 2 * H) + (ok ? lr : 0));
+    if (!ok) vb[j] = z4;
   }
   for (int j = lane; j < S16; j += 64) mk[j] = (j < S && mask[row0 + j]) ? 0.f : -INFINITY;
   __syncthreads();
@@ -577,20 +578,18 @@ attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restri
   for (int it = 0; it < NT; ++it)
 #pragma unroll
     for (int jt = 0; jt < NT; ++jt) c[it][jt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int d0 = 0; d0 < DH; d0 += 4) {
-    float a[NT], b[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      a[t] = Qs[(t * 16 + lr) * LD + d0 + lk];
-      b[t] = Ks[(t * 16 + lr) * LD + d0 + lk];
-    }
+  for (int u = 0; u < CU; ++u)
 #pragma unroll
-    for (int it = 0; it < NT; ++it)
+    for (int w = 0; w < 4; ++w)
 #pragma unroll
-      for (int jt = 0; jt < NT; ++jt)
-        c[it][jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[it], b[jt], c[it][jt], 0, 0, 0);
-  }
+      for (int it = 0; it < NT; ++it)
+#pragma unroll
+        for (int jt = 0; jt < NT; ++jt) {
+          const float a = w == 0 ? qa[it][u].x : w == 1 ? qa[it][u].y : w == 2 ? qa[it][u].z : qa[it][u].w;
+          const float b = w == 0 ? kb[jt][u].x : w == 1 ? kb[jt][u].y : w == 2 ? kb[jt][u].z : kb[jt][u].w;
+          c[it][jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c[it][jt], 0, 0, 0);
+        }
   // row softmax: row it*16 + 4 lk + r lives in the 16 lanes with this lk (column = jt*16 + lr)
   const float sq = sqrtf((float)DH);      // HF: scores / sqrt(head_size)
   float inv[NT][4];
@@ -619,27 +618,30 @@ attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restri
       inv[it][r] = sum > 0.f ? 1.f / sum : 0.f;
     }
   __syncthreads();
-  // O = P.V, per 16-column block of the head
+  // O = P.V: output block dt holds columns 4 lr + dt (lanes lr < DH / 4; DH = 32 leaves lanes
+  // 8-15 of each 16 idle in the 16-wide MFMA, their V operand zero)
 #pragma unroll
-  for (int dt = 0; dt < DH / 16; ++dt) {
+  for (int dt = 0; dt < 4; ++dt) {
     floatx4 o[NT];
 #pragma unroll
     for (int it = 0; it < NT; ++it) o[it] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j0 = 0; j0 < S16; j0 += 4) {
-      const float b = Vs[(j0 + lk) * LD + dt * 16 + lr];
+    for (int j = 0; j < JI; ++j) {
+      const float b = dt == 0 ? vb[j].x : dt == 1 ? vb[j].y : dt == 2 ? vb[j].z : vb[j].w;
 #pragma unroll
       for (int it = 0; it < NT; ++it)
-        o[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ps[(it * 16 + lr) * LP + j0 + lk], b, o[it], 0, 0, 0);
+        o[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ps[(it * 16 + lr) * LP + 4 * j + lk], b, o[it], 0, 0, 0);
     }
+    if (lr < VL) {
 #pragma unroll
-    for (int it = 0; it < NT; ++it)
+      for (int it = 0; it < NT; ++it)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = it * 16 + 4 * lk + r;
-        if (i < S)
-          store_act1<_Float16, true>(ctx + (row0 + i) * ld3, H, h * DH + dt * 16 + lr, o[it][r] * inv[it][r]);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int i = it * 16 + 4 * lk + r;
+          if (i < S)
+            store_act1<_Float16, true>(ctx + (row0 + i) * ld3, H, h * DH + 4 * lr + dt, o[it][r] * inv[it][r]);
+        }
+    }
   }
 }
 

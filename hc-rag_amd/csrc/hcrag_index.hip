@@ -425,7 +425,7 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       ix->opt_stride = value;
       return HCR_OK;
     case HCR_OPT_QS_FORM:
-      if (value < 0 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not in [0, 2]", value);
+      if (value < 0 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not in [0, 4]", value);
       ix->opt_qs = value;
       return HCR_OK;
     default:
@@ -524,7 +524,7 @@ static const TestHooks& hooks() {
 // qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h); qw1: the
 // one-wave-per-SIMD form (score_qw1.h), spread = its DMA issue spread over the MFMA groups
 struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false, nw8 = false, pipe = false,
-               qs4 = false; };
+               qs4 = false; int hs = 2; };
 // qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
 // QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1,
@@ -554,17 +554,25 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
   // vs 4.45, B = 256 4.52 vs 4.59; 1M x 384 B = 32 0.187 vs 0.295, B = 256 0.290 vs 0.331.
   if (nq <= hooks().qs_max) {
-    // QS4: 128-query 4-wave workgroups, two per CU (score_qs.h).  The default for 129-256
-    // queries (KS <= 12: configs[1]); HCR_OPT_QS_FORM = 2 also from 65, 1 never.  r03 A/B at
-    // 1M x 384, B = 256 (score ms): 0.2688 vs 0.2702 at stride 64, 0.2637 vs 0.2701 at 32.
-    if (opt_qs != 1 && nq > (opt_qs == 2 ? 64 : 128) && qs_supported(ld, 2)) {
+    // QS4 (HCR_OPT_QS_FORM = 2): 128-query 4-wave workgroups, two per CU (score_qs.h).  Not the
+    // default: r03 A/B at 1M x 384, B = 256 (score ms, two boxes): 0.2688 vs 0.2702 (8-wave) at
+    // stride 64, 0.2637 vs 0.2701 at 32; 0.2763 vs 0.2683 at 64, and the 8-wave form at 16 0.262.
+    if (opt_qs == 2 && nq > 64 && qs_supported(ld, 2)) {
       V3Cfg c{128, 128, 4, true};
       c.qs4 = true;
       return c;
     }
     // 129-256 queries with KS <= 12: one 256-query block on 128-row tiles (each row filled
     // into LDS once instead of once per 128-query block)
-    if (nq > 128 && qs_supported(ld, 2)) return {128, 256, 8, true};
+    if (nq > 128 && qs_supported(ld, 2)) {
+      V3Cfg c{128, 256, 8, true};
+      // KS = 12 (D = 384, configs[1]): 128-deep ring stages by default -- 3 barriers per 128-row
+      // tile instead of 6 (r03 A/B, 1M x 384, B = 256, score ms: 64-deep 0.2694, 128-deep
+      // 0.2536, 192-deep 0.2559; stamps: 14.1k -> 12.2k cycles per tile); HCR_OPT_QS_FORM 1 / 4:
+      // 64- / 192-deep
+      if (ld / V3_BK == 12 && opt_qs != 1) c.hs = opt_qs == 4 ? 6 : 4;
+      return c;
+    }
     // (KS = 24 without the UNIT epilogue spills VGPRs in its tile loop: v3/v4 then)
     if (qs_supported(ld, 1) && (unit_ok || ld / V3_BK < 24)) return {kQsRowTile, 128, 4, true};
   }
@@ -620,7 +628,7 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
            ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr, ix->w_qhat.p, a.nqb, a.P,
            a.nvt, a.tstride, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
-           (c.qt == 256 || c.qs4) ? 2 : 1, c.qs4 ? 4 : 8};
+           (c.qt == 256 || c.qs4) ? 2 : 1, c.qs4 ? 4 : 8, c.hs};
   return launch_qs(ix->dtype, q, st);
 }
 
@@ -804,9 +812,43 @@ seed_from_maxima_kernel(const float* __restrict__ umax, int U, int nqpad, int j,
     sv[i] = (v == v && v > -INFINITY) ? (uint64_t)ord32(v) : 0ull;   // NaN / -inf: no row
   }
   __syncthreads();
-  block_sort_desc_u64(sv, M);
+  block_sort_desc_u64_fast(sv, M);
   if (threadIdx.x == 0) {
     const uint32_t t = j <= U ? (uint32_t)sv[j - 1] : 0u;
+    tau_g[q] = t;
+    if (tau_est) tau_est[q] = t;
+  }
+}
+
+// The same seed with one wave per query and the U maxima in registers (E per lane, U <= 64 E):
+// the j-th largest ordered key is the largest t with #{v >= t} >= j, found bit by bit from the
+// top with ballot counts -- no LDS, no block barriers (the block sort above: 45 barrier-separated
+// stages for U = 306; r03 kernel trace at the W = 8 rank shape, 1024 queries: 16 us).  Invalid
+// maxima (NaN, -inf) are key 0, as there; fewer than j valid ones give 0.
+template <int E>
+__global__ void __launch_bounds__(256)
+seed_select_kernel(const float* __restrict__ umax, int U, int nqpad, int nq, int j,
+                   uint32_t* __restrict__ tau_g, uint32_t* __restrict__ tau_est) {
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  uint32_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = e * 64 + lane;
+    const float x = i < U ? umax[(size_t)i * nqpad + q] : -INFINITY;
+    v[e] = (x == x && x > -INFINITY) ? ord32(x) : 0u;
+  }
+  uint32_t t = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t c = t | (1u << bit);
+    int n = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) n += __popcll(__ballot(v[e] >= c));
+    if (n >= j) t = c;
+  }
+  if (j > U) t = 0u;
+  if (lane == 0) {
     tau_g[q] = t;
     if (tau_est) tau_est[q] = t;
   }
@@ -1026,10 +1068,19 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
         CHECK(ix->w_umax.ensure((size_t)U * nqpad * 4));
         if (ix->dtype == HCR_F16) CHECK(launch_v4_maxonly<_Float16>(ix, a, st));
         else CHECK(launch_v4_maxonly<__bf16>(ix, a, st));
-        const int M = next_pow2(U);
-        hipLaunchKernelGGL(seed_from_maxima_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 8, st,
-                           ix->w_umax.as<const float>(), U, nqpad, j, M, ix->w_taug.as<uint32_t>(),
-                           j < kp ? ix->w_tauest.as<uint32_t>() : nullptr);
+        uint32_t* te = j < kp ? ix->w_tauest.as<uint32_t>() : nullptr;
+        const dim3 gw((unsigned)((nq + 3) / 4));
+        const float* um = ix->w_umax.as<const float>();
+        uint32_t* tg = ix->w_taug.as<uint32_t>();
+        if (U <= 128) hipLaunchKernelGGL(seed_select_kernel<2>, gw, dim3(256), 0, st, um, U, nqpad, nq, j, tg, te);
+        else if (U <= 256) hipLaunchKernelGGL(seed_select_kernel<4>, gw, dim3(256), 0, st, um, U, nqpad, nq, j, tg, te);
+        else if (U <= 512) hipLaunchKernelGGL(seed_select_kernel<8>, gw, dim3(256), 0, st, um, U, nqpad, nq, j, tg, te);
+        else if (U <= 1024) hipLaunchKernelGGL(seed_select_kernel<16>, gw, dim3(256), 0, st, um, U, nqpad, nq, j, tg, te);
+        else {                                   // (the block sort for the largest samples)
+          const int M = next_pow2(U);
+          hipLaunchKernelGGL(seed_from_maxima_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 8, st,
+                             um, U, nqpad, j, M, tg, te);
+        }
         HIPC(hipGetLastError());
       } else {
         if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));

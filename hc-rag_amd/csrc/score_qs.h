@@ -98,11 +98,11 @@ __device__ __forceinline__ void qs_read_u32x8(uint32_t a, uint32_t (&w)[8]) {
   w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
-template <int NST, int KS, int RT_, int NQ, int NW = 8>
+template <int NST, int KS, int RT_, int NQ, int NW = 8, int HS = 2>
 struct QsLayout {
   static constexpr int RT = RT_, QT = 16 * NQ * NW;
-  static constexpr int SPT = KS / 2;                       // stages per tile (64-deep stages)
-  static constexpr int STAGE = RT * 128;                   // RT rows x 64 k: two 32-deep halves
+  static constexpr int SPT = KS / HS;                      // stages per tile (32 HS-deep stages)
+  static constexpr int STAGE = RT * 64 * HS;               // RT rows x 32 HS k: HS 32-deep halves
   // tile slots of inverse norms / bounds / mask words: a tile's slot must outlive the NST-1
   // stages of look-ahead, (NIS - 1) * SPT > NST - 1
   static constexpr int NIS = (NST - 1) / SPT + 2;
@@ -114,7 +114,7 @@ struct QsLayout {
   static constexpr int TAU = MSK + NIS * 64;               // u64 tau_key[QT]
   static constexpr int CNT = TAU + QT * 8;                 // int cnt[QT]
   static constexpr int TOTAL = CNT + QT * 4;
-  static_assert(KS % 2 == 0, "64-deep stages");
+  static_assert(KS % HS == 0, "whole stages per tile");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
@@ -131,22 +131,26 @@ struct QsLayout {
 // independent 4-wave workgroups drift apart, so one's epilogue runs under the other's MFMAs.
 // Rows are then filled into LDS once per 128 queries (the second query block's workgroup
 // reads them from the XCD's L2: consecutive workgroups of one XCD).
+//
+// HS: 32-deep k-steps per stage (2: 64-deep stages; 4 / 6 at configs[1]'s KS = 12: fewer
+// barriers per tile -- 3 or 2 instead of 6 -- each amortising the skew between the SIMD's two
+// waves and the fragment-read start-up over more MFMAs).
 template <typename TM, int CAP, int KS, bool UNIT, int NQ = 1, int RT_ = 256,
-          int NST = (RT_ == 256 ? 4 : 8), int NW = 8>
+          int NST = (RT_ == 256 ? 4 : 8), int NW = 8, int HS = 2>
 __global__ void __launch_bounds__(NW * 64, 8 / NW)
 score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = QsLayout<NST, KS, RT_, NQ, NW>;
+  using L = QsLayout<NST, KS, RT_, NQ, NW, HS>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int RT = L::RT, QT = L::QT, MT = RT / 16, D = NST - 1, SPT = L::SPT;
   constexpr int PPH = RT / 16;            // 1 KiB LDS-DMA pieces per 32-deep half of a stage
-  constexpr int PPW = 2 * PPH / NW;       // ... per wave per stage
-  static_assert((2 * PPH) % NW == 0, "stage pieces per wave");
-  constexpr int NG = MT / 2;              // groups of 4 row blocks per stage (2 halves)
+  constexpr int PPW = HS * PPH / NW;      // ... per wave per stage
+  static_assert((HS * PPH) % NW == 0, "stage pieces per wave");
+  constexpr int NG = MT / 4 * HS;         // groups of 4 row blocks per stage (HS halves)
   static_assert(CAP >= 2 * RT, "candidate buffer must hold a tile's appends after a compaction");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -217,7 +221,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int j = wave + NW * i;           // piece: half j / PPH, rows (j % PPH) * 16 ..
-      dma16(a_rsrc, sa + j * 1024, voff, (j % PPH) * 16 * ldb + (2 * SP2 + j / PPH) * (V3_BK * 2));
+      dma16(a_rsrc, sa + j * 1024, voff, (j % PPH) * 16 * ldb + (HS * SP2 + j / PPH) * (V3_BK * 2));
     }
     if constexpr (SP2 == 0) {
       const int is = vt % L::NIS;
@@ -293,7 +297,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         issue_stage(std::integral_constant<int, (SP + D) % SPT>{}, vt + (SP + D) / SPT, (s + D) % NST);
       const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(
           (int)(lds0 + (uint32_t)((s % NST) * L::STAGE)));
-      // NG groups of 4 row blocks (2 halves x MT/4), group j+1's reads in flight under group
+      // NG groups of 4 row blocks (HS halves x MT/4), group j+1's reads in flight under group
       // j's MFMAs
       constexpr int GPH = MT / 4;
       V av[2][4];
@@ -312,7 +316,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int n = 0; n < NQ; ++n)
-            acc[g4 * 4 + i][n] = Op::run(av[j & 1][i], qf[n][2 * SP + h], acc[g4 * 4 + i][n]);
+            acc[g4 * 4 + i][n] = Op::run(av[j & 1][i], qf[n][HS * SP + h], acc[g4 * 4 + i][n]);
       }
 #ifdef HCR_QS_STAMPS
       HCR_QS_STAMP(st_t2);

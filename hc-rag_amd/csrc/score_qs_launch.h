@@ -22,6 +22,8 @@ struct QsArgs {
                              // QW1: its tuning shape (HCR_OPT_QW1_SHAPE)
   int nw = 8;                // QS waves per workgroup: 8, or 4 with nq_blocks 2 (QS4: two
                              // 128-query workgroups per CU)
+  int hs = 2;                // 32-deep k-steps per ring stage (2; 4 or 6 for the 8-wave
+                             // 256-query form at KS = 12)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128

@@ -576,7 +576,7 @@ __device__ __forceinline__ int merge_block_lds(const uint64_t* __restrict__ list
   while (m < cs || m < kp) m <<= 1;                   // <= G * kp (host sizes the LDS)
   for (int i = cs + t; i < m; i += blockDim.x) sm_keys[i] = 0ull;
   __syncthreads();
-  block_sort_desc_u64(sm_keys, m);
+  block_sort_desc_u64_fast(sm_keys, m);
   return cs;
 }
 
@@ -698,7 +698,7 @@ __device__ __forceinline__ void rescore_block(const uint64_t* keys, const double
     }
   }
   __syncthreads();
-  block_sort_desc_pair(hi, lo, kp);
+  block_sort_desc_pair_fast(hi, lo, kp);
   const int nvalid = *s_nvalid;
   if (threadIdx.x == 0) {
     // Every row outside the candidates has coarse score <= B: the k'-th candidate's coarse
@@ -1079,7 +1079,7 @@ exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
     lo[i] = v ? buf_lo[(size_t)q * cap + i] : 0ull;
   }
   __syncthreads();
-  block_sort_desc_pair(hi, lo, m);
+  block_sort_desc_pair_fast(hi, lo, m);
   if (c > (unsigned int)cap) {
     if (threadIdx.x == 0) {
       // (a) the histogram: top bins down to the one where k rows are reached (the admitted
@@ -1180,7 +1180,7 @@ merge_shards_kernel(const double* __restrict__ s, const int64_t* __restrict__ id
     lo[i] = l;
   }
   __syncthreads();
-  block_sort_desc_pair(hi, lo, M);
+  block_sort_desc_pair_fast(hi, lo, M);
   for (int t = threadIdx.x; t < k; t += blockDim.x) {
     const bool ok = hi[t] != 0ull;
     out_s[q * k + t] = ok ? unord64(hi[t]) : -INFINITY;

@@ -188,7 +188,8 @@ class VectorIndex:
         ``VectorIndex.OPT_QW1``: -1 heuristic, 0 never QW1, 1 QW1 (DMA spread), 2 QW1 (DMA at
         the stage barrier), 3 / 4 the same in the 8-wave form where it exists (D = 384).
         ``VectorIndex.OPT_SAMPLE_STRIDE``: the sampling pre-pass's row-tile stride (0 heuristic).
-        ``VectorIndex.OPT_QS_FORM``: 0 heuristic, 1 the 8-wave QS, 2 QS4 (D <= 384, 65-256 queries)."""
+        ``VectorIndex.OPT_QS_FORM``: 0 heuristic, 1 the 8-wave QS, 2 QS4 (D <= 384, 65-256 queries),
+        3 / 4 the 8-wave QS with 128- / 192-deep ring stages (D = 384, 129-256 queries)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
 

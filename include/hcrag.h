@@ -171,9 +171,10 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                gives a tighter seed (fewer candidate appends in the dense pass) at the cost of
  *                a longer pre-pass.
  *   HCR_OPT_QS_FORM: the query-stationary kernel's form for 65-256 queries at D <= 384: 0 = the
- *                heuristic (QS4 from 129 queries), 1 = never QS4 (one 8-wave workgroup per CU:
- *                256 queries on 128-row tiles from 129 queries), 2 = QS4 from 65 queries
- *                (128-query 4-wave workgroups, two per CU). */
+ *                heuristic (= 3 at D = 384), 1 = one 8-wave workgroup per CU (256 queries on
+ *                128-row tiles from 129 queries) with 64-deep ring stages, 2 = QS4 from 65
+ *                queries (128-query 4-wave workgroups, two per CU), 3 / 4 = the 8-wave form with
+ *                128- / 192-deep ring stages (D = 384 only, 129-256 queries). */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3,
                HCR_OPT_QS_FORM = 4 } hcr_index_option;
 int hcr_index_set_option(hcr_index* index, int option, int value);

@@ -1,6 +1,8 @@
-"""GPU parity of QS4 (score_qs.h with NW = 4: two 128-query 4-wave workgroups per CU, each with
-its own barrier), asked for with HCR_OPT_QS_FORM = 2, on the shapes it takes (D <= 384, 65-256
-queries): L2-normalised (UNIT epilogue) and raw corpora, a row mask, bf16.  Ids are compared
+"""GPU parity of the query-stationary kernel's forms (HCR_OPT_QS_FORM): QS4 (score_qs.h with
+NW = 4: two 128-query 4-wave workgroups per CU, each with its own barrier; form 2) on the shapes
+it takes (D <= 384, 65-256 queries), and the 8-wave 256-query form with 128- / 192-deep ring
+stages (HS = 4 / 6; forms 3 / 4, D = 384, 129-256 queries): L2-normalised (UNIT epilogue) and
+raw corpora, a row mask, bf16.  Ids are compared
 EXACTLY with the fp64 oracle and scores to 1e-12; the stats must show that QS4 ran
 (score_kernel 10), so a silent reroute fails.  Reference: experiments/main.py:841-844
 (cosine_similarity + argsort[::-1][:k]) and :872-885 (the category filter)."""
@@ -12,6 +14,7 @@ from oracle import cosine_topk as O
 pytestmark = pytest.mark.gpu
 
 QS4 = 10         # hcr_search_stats.score_kernel of QS4
+QS = 5           # ... of the 8-wave form (any stage depth)
 
 
 @pytest.fixture(scope="module")
@@ -31,25 +34,27 @@ def _planted(rng, E, B, noise=0.2):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("D", [128, 192, 384])
+@pytest.mark.parametrize("D,form", [(128, 2), (192, 2), (384, 2), (384, 3), (384, 4)])
 @pytest.mark.parametrize("B,k", [(65, 10), (200, 10), (256, 32)])
 @pytest.mark.parametrize("normalize", [True, False])
-def test_qs4_parity(hc, dtype, D, B, k, normalize):
+def test_qs4_parity(hc, dtype, D, form, B, k, normalize):
     """N not a multiple of the 128-row tile, tens of tiles per workgroup (the seeded pre-pass
     runs), a padded second query block (65, 200), the UNIT and the inverse-norm epilogues."""
-    rng = np.random.default_rng(D * 7 + B + k + int(normalize))
+    if form != 2 and B <= 128:
+        pytest.skip("the deep-stage 8-wave forms take 129-256 queries")
+    rng = np.random.default_rng(D * 7 + B + k + int(normalize) + form)
     N = 120000 + 77
     E = rng.standard_normal((N, D)).astype(np.float32)
     if not normalize:
         E *= rng.uniform(0.5, 2.0, (N, 1)).astype(np.float32)
     Q, src = _planted(rng, E, B)
     with hc.VectorIndex(D, dtype) as ix:
-        ix.set_option(ix.OPT_QS_FORM, 2)
+        ix.set_option(ix.OPT_QS_FORM, form)
         ix.add(E, normalize=normalize)
         R = ix.get_rows()
         s, i = ix.search(Q, k)
         st = ix.last_stats()
-        assert st["score_kernel"] == QS4, st
+        assert st["score_kernel"] == (QS4 if form == 2 else QS), st
         assert st["uncertified_queries"] == 0, st
     sub = np.r_[0:16, B // 2: B // 2 + 16, B - 8:B]
     es, ei = O.cosine_topk(Q[sub], R, k)
