@@ -437,10 +437,14 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
         const uint64_t key = make_key(sc, rowl);
         if (key > tkr[n]) {
+#ifndef HCR_QS_NOAPPEND   // (diagnostic stamps builds only: what the appends / their stores cost)
           const int ql = qlane + 16 * n;
           const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+#ifndef HCR_QS_NOSTORE
           wbuf[(size_t)ql * CAP + pos] = key;
+#endif
           need |= pos + 1 > CAP - RT;
+#endif
         }
       };
 #pragma unroll
