@@ -524,7 +524,9 @@ def test_configs4_rank_shape_bf16(hc):
         ix.search_device(q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(),
                          stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        assert ix.last_stats()["uncertified_queries"] == 0
+        st = ix.last_stats()
+        assert st["uncertified_queries"] == 0, st
+        assert st["score_kernel"] == 7, st            # QW1, the D = 1024 large-batch kernel
         S, I = S.cpu().numpy(), I.cpu().numpy()
         R = ix.get_rows()
     assert np.mean(I[::2, 0] - 3 * N == planted) > 0.99
