@@ -66,6 +66,7 @@ struct hcr_index {
   int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
   int opt_qs = 0;               // HCR_OPT_QS_FORM (0: the heuristic)
+  int opt_prepass = 0;          // HCR_OPT_PREPASS (0: the heuristic)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -423,6 +424,10 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       if (value != 0 && (value < 2 || value > 4096))
         return set_err(HCR_EINVAL, "HCR_OPT_SAMPLE_STRIDE value %d not 0 or in [2, 4096]", value);
       ix->opt_stride = value;
+      return HCR_OK;
+    case HCR_OPT_PREPASS:
+      if (value < 0 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_PREPASS value %d not in [0, 2]", value);
+      ix->opt_prepass = value;
       return HCR_OK;
     case HCR_OPT_QS_FORM:
       if (value < 0 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not in [0, 4]", value);
@@ -1066,7 +1071,16 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       if (maxonly) {
         const int U = 2 * a.nvt;
         CHECK(ix->w_umax.ensure((size_t)U * nqpad * 4));
-        if (ix->dtype == HCR_F16) CHECK(launch_v4_maxonly<_Float16>(ix, a, st));
+        // the sampled tiles on QW when the dense pass is QW (its MAXONLY form, score_qw.h; r03:
+        // v4's form is LDS-fill-bound), on v4 otherwise; HCR_OPT_PREPASS 1 / 2 force v4 / QW
+        if (qw && ix->opt_prepass != 1) {
+          QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, nqb_pre,
+                   a.P, a.nvt * (256 / qw_rows(ix->ld)), a.tstride, ix->w_buf.as<uint64_t>(),
+                   ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), kp, cap,
+                   true, 0};
+          q.umax = ix->w_umax.as<float>();
+          CHECK(launch_qw(ix->dtype, q, st));
+        } else if (ix->dtype == HCR_F16) CHECK(launch_v4_maxonly<_Float16>(ix, a, st));
         else CHECK(launch_v4_maxonly<__bf16>(ix, a, st));
         uint32_t* te = j < kp ? ix->w_tauest.as<uint32_t>() : nullptr;
         const dim3 gw((unsigned)((nq + 3) / 4));

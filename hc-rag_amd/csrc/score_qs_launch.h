@@ -24,6 +24,8 @@ struct QsArgs {
                              // 128-query workgroups per CU)
   int hs = 2;                // 32-deep k-steps per ring stage (2; 4 or 6 for the 8-wave
                              // 256-query form at KS = 12)
+  float* umax = nullptr;     // QW: the MAXONLY sampling pre-pass into umax[unit][nqb * 256]
+                             // (ntiles = virtual stages of the sampled tiles, tstride their stride)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128

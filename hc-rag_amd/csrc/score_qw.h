@@ -88,12 +88,17 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
   return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
 }
 
-template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST>
+// MAXONLY: the sampling pre-pass on QW (DESIGN.md §4 "Estimated seed"): ntiles counts virtual
+// stages of the sampled 256-row tiles (tile vt * tstride, 256 / SR stages each), partitions are
+// whole 128-row units, and per unit and query the largest coarse score goes to
+// umax[unit][nqb * QT] -- no candidate lists (v4's MAXONLY form is LDS-fill-bound).
+template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp,
+                     int tstride = 1, float* __restrict__ umax = nullptr) {
   using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
@@ -114,8 +119,14 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int qb = g % nqb, p = g / nqb;
-  const int t0 = (int)((int64_t)p * ntiles / P);
-  const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
+  constexpr int SPT8 = 256 / SR;                      // stages per sampled 256-row tile
+  constexpr int SPU = 128 / SR;                       // stages per 128-row unit (MAXONLY)
+  const int t0 = MAXONLY ? (int)((int64_t)p * (ntiles / SPU) / P) * SPU : (int)((int64_t)p * ntiles / P);
+  const int t1 = MAXONLY ? (int)((int64_t)(p + 1) * (ntiles / SPU) / P) * SPU : (int)((int64_t)(p + 1) * ntiles / P);
+  // a virtual stage's row stage (MAXONLY: of sampled tile vs / SPT8)
+  auto real_stage = [&](int vs) __attribute__((always_inline)) {
+    return MAXONLY ? (int64_t)(vs / SPT8) * tstride * SPT8 + vs % SPT8 : (int64_t)vs;
+  };
   const int qbase = qb * QT;
   uint64_t* wbuf = buf + (size_t)b * QT * CAP;
   const int wq0 = wave * 32;                          // this wave's first query (block-local)
@@ -123,7 +134,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   if (lane < 32) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
   if (t0 >= t1) {
-    if (lane < 32) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
+    if (!MAXONLY && lane < 32) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
     return;
   }
 
@@ -155,7 +166,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const bool live = i < nsteps;
     StageDesc d;
     d.slot = __builtin_amdgcn_readfirstlane(i % NST);
-    const int tile = __builtin_amdgcn_readfirstlane(t0 + (live ? i : 0));
+    const int64_t tile = real_stage(__builtin_amdgcn_readfirstlane(t0 + (live ? i : 0)));
     d.a = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(rows_b + (size_t)tile * SR * ldb), (short)0,
                                             live ? SR * ldb : 0, 0x00020000);
     d.t = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(tau_g + qbase), (short)0, live ? QT * 4 : 0,
@@ -188,6 +199,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   bool need = false;
   uint64_t tkr[2] = {0ull, 0ull};
+  float umx[2] = {0.f, 0.f};                         // MAXONLY: the current unit's maxima
   for (int s = 0; s < nsteps; ++s) {
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
@@ -255,13 +267,35 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
     const int lq = le >> 4;
     const int qle = wq0 + (le & 15);                 // the query of accumulator block 0
-    const int64_t row0 = (int64_t)(t0 + s) * SR;
+    const int64_t row0 = real_stage(t0 + s) * SR;
     if (row0 + SR > n_rows) {      // the corpus' last tile: rows past the end never pass (NaN)
 #pragma unroll
       for (int m = 0; m < RB; ++m)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (row0 + m * 16 + lq * 4 + r >= n_rows) acc[m][0][r] = acc[m][1][r] = __builtin_nanf("");
+    }
+    if constexpr (MAXONLY) {
+      // per query: the largest of the stage's SR rows (the lane's RB x 4, then over the 4
+      // row-group lanes l, l ^ 16, l ^ 32, l ^ 48), folded into the unit's maximum; a quiet NaN
+      // (rows past the corpus) never wins a maximum unless every operand is one
+      const int vs = t0 + s;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        float mx = qw_max4(acc[0][n]);
+#pragma unroll
+        for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        umx[n] = (vs % SPU == 0) ? mx : fmaxf(umx[n], mx);
+      }
+      if (vs % SPU == SPU - 1 && lane < 16) {
+        const int u = (vs / SPT8) * 2 + (vs % SPT8) / SPU;
+        float* dst = umax + (size_t)u * ((size_t)nqb * QT) + qbase + qle;
+        dst[0] = umx[0];
+        dst[16] = umx[1];
+      }
+      continue;
     }
     float thr[2];
     thr[0] = fmaxf(tkr[0] ? key_score(tkr[0]) : -INFINITY, unord32(tg2[0]));
@@ -319,6 +353,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   }
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (MAXONLY) return;
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 32, kp, lane, partials, pcnt, P, p);
 }

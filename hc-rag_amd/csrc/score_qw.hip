@@ -14,9 +14,14 @@ namespace {
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                     static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+  if (a.umax)       // the sampling pre-pass (MAXONLY)
+    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
+                       st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, a.tstride, a.umax);
+  else
+    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                       static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP>

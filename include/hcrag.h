@@ -174,9 +174,11 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                heuristic (= 3 at D = 384), 1 = one 8-wave workgroup per CU (256 queries on
  *                128-row tiles from 129 queries) with 64-deep ring stages, 2 = QS4 from 65
  *                queries (128-query 4-wave workgroups, two per CU), 3 / 4 = the 8-wave form with
- *                128- / 192-deep ring stages (D = 384 only, 129-256 queries). */
+ *                128- / 192-deep ring stages (D = 384 only, 129-256 queries).
+ *   HCR_OPT_PREPASS: the sampling pre-pass kernel when the dense pass runs on QW: 0 = the
+ *                heuristic, 1 = the 256 x 256 v4 kernel's MAXONLY form, 2 = QW's MAXONLY form. */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3,
-               HCR_OPT_QS_FORM = 4 } hcr_index_option;
+               HCR_OPT_QS_FORM = 4, HCR_OPT_PREPASS = 5 } hcr_index_option;
 int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)

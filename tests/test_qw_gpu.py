@@ -163,3 +163,30 @@ def test_qw_cold_and_aggressive_seeds(env):
                        env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "cold ok" in r.stdout
+
+
+@pytest.mark.parametrize("D,N", [(384, 400000 + 3), (768, 300000 + 11)])
+def test_qw_maxonly_prepass_forms_agree(hc, D, N):
+    """The sampling pre-pass on QW's MAXONLY form (HCR_OPT_PREPASS 2, the default under QW) and
+    on v4's (1): N not a multiple of the 256-row sampled tile (the last unit ends past the
+    corpus: NaN rows), several partitions of whole 128-row units; the seeds only steer which
+    rows are appended, so both give ids identical to the oracle and identical scores."""
+    rng = np.random.default_rng(D + 7)
+    B, k = 512, 16
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    Q = _planted(rng, E, B)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        out = {}
+        for form in (2, 1, 0):
+            ix.set_option(ix.OPT_PREPASS, form)
+            out[form] = ix.search(Q, k)
+            st = ix.last_stats()
+            assert st["score_kernel"] == QW and st["uncertified_queries"] == 0, st
+    for form in (1, 0):
+        np.testing.assert_array_equal(out[form][1], out[2][1])
+        np.testing.assert_array_equal(out[form][0], out[2][0])
+    sub = np.r_[0:12, B - 12:B]
+    es, ei = O.cosine_topk(Q[sub], R, k)
+    _check(out[2][0][sub], out[2][1][sub], es, ei)

@@ -49,11 +49,12 @@ def main():
         ref = None
         for r in range(a.rounds):
             for vs in a.variants.split(","):
-                v, shape, stride, qsf = (int(x) for x in (vs + ":0:0:0").split(":")[:4])
+                v, shape, stride, qsf, pre = (int(x) for x in (vs + ":0:0:0:0").split(":")[:5])
                 ix.set_option(ix.OPT_QW1, v)
                 ix.set_option(ix.OPT_QW1_SHAPE, shape)
                 ix.set_option(ix.OPT_SAMPLE_STRIDE, stride)
                 ix.set_option(ix.OPT_QS_FORM, qsf)
+                ix.set_option(ix.OPT_PREPASS, pre)
                 ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
                 torch.cuda.synchronize()
                 ix.set_timing(True)
