@@ -690,7 +690,7 @@ def main():
              7: "score_topk_qw1_kernel (one wave per SIMD, 64 / 48 queries per wave in AGPR/VGPRs)",
              8: "score_topk_qw1_kernel (8-wave form)",
              9: "score_topk_qw1p_kernel (QW1 software-pipelined)"}.get(st.get("score_kernel", 0), "?")
-    roof["kernel"] = (kname + ", fused MFMA score + top-k': sample pre-pass (v4 MAXONLY) + dense "
+    roof["kernel"] = (kname + ", fused MFMA score + top-k': sampling pre-pass (MAXONLY form: QW's under QW, else v4's) + dense "
                       "pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
     roof["flops_per_launch"] = flops
