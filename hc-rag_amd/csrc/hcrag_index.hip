@@ -776,7 +776,7 @@ static constexpr int kSampleStrideDefault = 512;  // pre-pass samples 1 row tile
 // MAXONLY pre-pass stride: the largest power of two in [16, 128] that keeps >= 150 row tiles
 // (~38k rows) in the sample.  The seed's global rank is ~j / (sampled fraction) (j = 8-25, see
 // search_pass): a small corpus needs a denser sample for a seed tight enough to keep the dense
-// pass's appends rare, a large one reaches it at 128.  r03 A/B (tools/r03_seed.sh, score ms):
+// pass's appends rare, a large one reaches it at 128.  r03 A/B (tools/rounds/r03_seed.sh, score ms):
 // 1M x 384 B = 256 stride 64 0.270 / 32 0.264 / 16 0.260 (QS4); 1.25M x 768 B = 1024 (the W = 8
 // rank shape) 64 1.746 / 32 1.712 / 16 1.723 / 8 1.873; 2.5M x 768 64 3.427 / 32 3.431 / 16
 // 3.635; 10M x 768 128 13.20 / 64 13.23 / 32 13.48.
