@@ -73,6 +73,11 @@ def parse():
                    help="skip the configs[1] leg (1M x 384 f16, B = 256, top-10; 1 GPU)")
     p.add_argument("--no-vendor-gemm", action="store_true",
                    help="skip the vendor-GEMM calibration of the MFMA roofline (torch.mm)")
+    p.add_argument("--power-seconds", type=float, default=3.0,
+                   help="seconds of back-to-back headline steps with board power / clock sampled "
+                        "(0: skip)")
+    p.add_argument("--large-k", default="1000,2048",
+                   help="k values of the k > 256 leg (exact fallback) at B = 64 ('' to skip)")
     p.add_argument("--no-configs4", action="store_true",
                    help="skip the configs[4] per-rank leg (12.5M x 1024 bf16, 8192 queries, "
                         "top-64, bge-large encoder; 1 GPU)")
@@ -107,12 +112,29 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cgroup_cpu_quota():
+    """CPUs of this process' cgroup quota (cgroup v2 cpu.max 'quota period'), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_cores():
-    """Host threads the CPU legs actually ran on: the BLAS / OpenMP thread count, capped by the
-    CPUs this process may run on (sched_getaffinity; the box's machine-wide count is larger)."""
-    aff = len(os.sched_getaffinity(0))
+    """Host threads the CPU legs run on: the CPUs this process may run on (sched_getaffinity),
+    capped by the cgroup quota and by the pool's per-GPU host-CPU share, which the GPU box
+    states in OMP_NUM_THREADS (16 per GPU there; sched_getaffinity shows the whole machine's
+    CPUs, shared with the other GPUs' jobs)."""
+    n = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    if quota:
+        n = min(n, max(1, int(quota)))
     env = os.environ.get("OMP_NUM_THREADS") or os.environ.get("OPENBLAS_NUM_THREADS")
-    return min(aff, int(env)) if env and env.isdigit() and int(env) > 0 else aff
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n
 
 
 def make_shard(ix, hc, r0, r1, dim, dtype, dev, seed=1000, chunk=1 << 20):
@@ -181,37 +203,193 @@ def cpu_baseline(E_rows_f16, Q, k, n_total):
     cosine in fp64 over the fp64 matrix + np.argsort(...)[::-1][:k] (experiments/main.py:
     841-844) -- on a bounded sample, extrapolated linearly in rows; beside it the tuned CPU
     path of BASELINE.md §3 (fp32 BLAS GEMM + argpartition) on the same sample."""
+    from concurrent.futures import ThreadPoolExecutor
+    from threadpoolctl import threadpool_limits
     from oracle import cosine_topk as O
+    threads = cpu_cores()
     E = E_rows_f16.astype(np.float64)
     q = Q.astype(np.float64)
-    t0 = time.perf_counter()
-    sims = O.cosine_similarity64(q, E)
-    top = np.argsort(sims, axis=1)[:, ::-1][:, :k]
-    t = time.perf_counter() - t0
-    del top, sims
-    nq, nr = Q.shape[0], E.shape[0]
-    qps = nq / (t * (n_total / nr))
-    # tuned: fp32 unit rows (normalised once, outside the timed region, as an index would
-    # store them), one SGEMM, argpartition + a sort of the k survivors
-    E32 = (E / np.linalg.norm(E, axis=1, keepdims=True)).astype(np.float32)
-    q32 = Q.astype(np.float32)
-    del E
-    t1 = time.perf_counter()
-    s32 = (q32 / np.linalg.norm(q32, axis=1, keepdims=True)) @ E32.T
-    part = np.argpartition(-s32, k, axis=1)[:, :k]
-    np.take_along_axis(s32, part, axis=1).argsort(axis=1)
-    tt = time.perf_counter() - t1
-    del s32, E32
-    return {"value": qps, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
+    with threadpool_limits(limits=threads):          # BLAS threads = every CPU the job may use
+        t0 = time.perf_counter()
+        sims = O.cosine_similarity64(q, E)
+        top = np.argsort(sims, axis=1)[:, ::-1][:, :k]
+        t = time.perf_counter() - t0
+        del top, sims
+        nq, nr = Q.shape[0], E.shape[0]
+        qps = nq / (t * (n_total / nr))
+        # tuned: fp32 unit rows (normalised once, outside the timed region, as an index would
+        # store them), one SGEMM, argpartition + a sort of the k survivors -- the selection
+        # spread over the same threads (numpy releases the GIL in its partition / sort)
+        E32 = (E / np.linalg.norm(E, axis=1, keepdims=True)).astype(np.float32)
+        q32 = Q.astype(np.float32)
+        del E
+
+        def select(s32, a, b):
+            part = np.argpartition(-s32[a:b], k, axis=1)[:, :k]
+            np.take_along_axis(s32[a:b], part, axis=1).argsort(axis=1)
+        with ThreadPoolExecutor(threads) as pool:
+            t1 = time.perf_counter()
+            s32 = (q32 / np.linalg.norm(q32, axis=1, keepdims=True)) @ E32.T
+            step = -(-nq // threads)
+            list(pool.map(lambda a: select(s32, a, min(nq, a + step)), range(0, nq, step)))
+            tt = time.perf_counter() - t1
+        del s32, E32
+    return {"value": qps, "unit": "queries/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "threads_env": {v: os.environ.get(v) for v in (
                 "OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")},
-            "affinity_cpus": len(os.sched_getaffinity(0)),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "threads_rule": "BLAS threads and the tuned leg's selection threads = the CPUs the job "
+                            "may use: sched_getaffinity capped by the cgroup quota and by the pool's "
+                            "per-GPU host-CPU share (OMP_NUM_THREADS on the GPU box); the literal "
+                            "leg's argsort is numpy's own (single-threaded), as the reference runs it",
             "sample": f"{nq} queries x {nr:,}-row slice of the same corpus (fp16 decoded to fp64), "
                       f"cosine_similarity fp64 + argsort[::-1][:{k}] in {t:.2f} s, "
                       f"extrapolated linearly to {n_total:,} rows",
             "tuned": {"value": nq / (tt * (n_total / nr)), "unit": "queries/s",
                       "path": "fp32 SGEMM over pre-normalised rows + argpartition (BASELINE.md §3)",
                       "seconds_on_sample": round(tt, 3)}}
+
+
+class PowerSampler:
+    """Board power and gfx clock of one GPU from its amdgpu hwmon sysfs files, sampled by a
+    thread of this process (file reads only: no SMI child process).  power1_average /
+    power1_input are microwatts; freq1_input (label sclk) is Hz; pp_dpm_sclk's starred level is
+    the fallback clock.  The in-kernel clock reads up to ~10 % below these (MI355X_MICROARCH.md
+    'DVFS give-back' item 6); this samples what the board reports while the step runs."""
+
+    def __init__(self, dev_index, period=0.02):
+        import glob
+        import threading
+        self.period = period
+        self.samples = []
+        self._stop = threading.Event()
+        self._thread = None
+        self.dir = None
+        try:
+            pr = torch.cuda.get_device_properties(dev_index)
+            bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+            cands = [f"/sys/bus/pci/devices/{bdf}"]
+        except Exception:
+            cands = []
+        cands += sorted(glob.glob("/sys/class/drm/card*/device"))
+        for d in cands:
+            hw = sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*")))
+            if hw and any(os.path.exists(os.path.join(hw[0], f)) for f in ("power1_average", "power1_input")):
+                self.dir, self.hwmon = d, hw[0]
+                break
+
+    @staticmethod
+    def _read(path):
+        try:
+            with open(path) as fh:
+                return fh.read()
+        except OSError:
+            return None
+
+    def sample(self):
+        if not self.dir:
+            return None
+        w = None
+        for f in ("power1_average", "power1_input"):
+            v = self._read(os.path.join(self.hwmon, f))
+            if v and v.strip().isdigit() and int(v) > 0:
+                w = int(v) / 1e6
+                break
+        mhz = None
+        v = self._read(os.path.join(self.hwmon, "freq1_input"))
+        if v and v.strip().isdigit():
+            mhz = int(v) / 1e6
+        else:
+            txt = self._read(os.path.join(self.dir, "pp_dpm_sclk")) or ""
+            for ln in txt.splitlines():
+                if ln.strip().endswith("*"):
+                    try:
+                        mhz = float(ln.split(":")[1].strip().rstrip("*").strip().lower().rstrip("mhz"))
+                    except (IndexError, ValueError):
+                        pass
+        return (w, mhz)
+
+    def _run(self):
+        while not self._stop.is_set():
+            x = self.sample()
+            if x:
+                self.samples.append(x)
+            self._stop.wait(self.period)
+
+    def start(self):
+        import threading
+        self.samples = []
+        self._stop.clear()
+        self._thread = threading.Thread(target=self._run, daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        if self._thread:
+            self._thread.join()
+        ws = sorted(w for w, _ in self.samples if w is not None)
+        ms = sorted(m for _, m in self.samples if m is not None)
+        med = lambda xs: xs[len(xs) // 2] if xs else None
+        return {"samples": len(self.samples), "power_W_med": med(ws), "power_W_max": ws[-1] if ws else None,
+                "gfx_mhz_med": med(ms), "gfx_mhz_min": ms[0] if ms else None,
+                "source": (self.hwmon if self.dir else "no amdgpu hwmon in sysfs")}
+
+
+def power_leg(step, dev, achieved_tf, seconds=3.0):
+    """Board power and gfx clock while the headline step runs back to back for `seconds`
+    (after the timed region, same process, same shapes): is the dense pass at the board's power
+    cap, and what fraction of the MFMA peak AT THE HELD CLOCK does it reach (2.5 PF is quoted at
+    2400 MHz)?"""
+    ps = PowerSampler(dev.index)
+    step()
+    torch.cuda.synchronize()
+    ps.start()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds:
+        step()
+        n += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = ps.stop()
+    out["steps"] = n
+    out["ms_per_step"] = round(el / n * 1e3, 3)
+    mhz = out.get("gfx_mhz_med")
+    if mhz and achieved_tf:
+        peak_at = MFMA_PEAK_TFLOPS * mhz / 2400.0
+        out["mfma_peak_at_held_clock_TFLOPs"] = round(peak_at, 1)
+        out["frac_at_held_clock"] = round(achieved_tf / peak_at, 4)
+    return out
+
+
+def large_k_leg(ix, dev, nloc, D, B=64, ks=(1000, 2048), reps=3):
+    """k > 256 (no MFMA candidate path that deep: the exact fallback, MFMA-prefiltered scans of
+    the whole shard): ms per batch, fallback rounds, and the scans' bytes (rounds x
+    corpus) as a fraction of the 8 TB/s HBM roof.  experiments/main.py:844 (argsort has no k
+    cliff)."""
+    out = []
+    stream = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device=dev).manual_seed(31)
+    Q = torch.randn((B, D), device=dev, generator=g)
+    for k in ks:
+        S = torch.empty((B, k), dtype=torch.float64, device=dev)
+        I = torch.empty((B, k), dtype=torch.int64, device=dev)
+        ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        te = (time.perf_counter() - t0) / reps
+        st = ix.last_stats()
+        scan_bytes = st["fallback_rounds"] * nloc * D * 2
+        out.append({"batch": B, "k": k, "ms_per_batch": round(te * 1e3, 3),
+                    "fallback_queries": st["fallback_queries"], "fallback_rounds": st["fallback_rounds"],
+                    "scan_GB": round(scan_bytes / 1e9, 2),
+                    "hbm_frac_scan": round(scan_bytes / te / 1e9 / HBM_PEAK_GBS, 4)})
+        log(json.dumps({"large_k": out[-1]}))
+        del S, I
+    return out
 
 
 ENC_SHAPES = {
@@ -687,9 +865,8 @@ def main():
              5: "score_topk_qs_kernel (query-stationary, 128/256 queries per workgroup)",
              6: "score_topk_qw_kernel (wide query-stationary: 256 queries per workgroup in VGPRs, "
                 "full-K row stages)",
-             7: "score_topk_qw1_kernel (one wave per SIMD, 64 / 48 queries per wave in AGPR/VGPRs)",
-             8: "score_topk_qw1_kernel (8-wave form)",
-             9: "score_topk_qw1p_kernel (QW1 software-pipelined)"}.get(st.get("score_kernel", 0), "?")
+             7: "score_topk_qw1_kernel (D = 1024: one wave per SIMD, 48 queries per wave in AGPR/VGPRs)"
+             }.get(st.get("score_kernel", 0), "?")
     roof["kernel"] = (kname + ", fused MFMA score + top-k': sampling pre-pass (MAXONLY form: QW's under QW, else v4's) + dense "
                       "pass, HIP events around both on the library's stream")
     roof["kernel_ms_avg"] = round(avg_ms, 4)
@@ -711,6 +888,9 @@ def main():
         roof["lds_dma_fill_TBps"] = round(fill / (avg_ms * 1e-3) / 1e12, 2)
 
     value = nq / (elapsed / a.steps)
+    if a.power_seconds > 0 and roof["bound"] == "mfma" and world == 1:
+        roof["power_clock"] = power_leg(step, dev, achieved, a.power_seconds)
+        log(json.dumps({"power_clock": roof["power_clock"]}))
     if rank == 0 and world == 1 and not a.no_vendor_gemm and roof["bound"] == "mfma":
         cal = vendor_gemm_leg(dev)
         cal["this_kernel_vs_headline_shape"] = round(
@@ -741,6 +921,9 @@ def main():
     sweep = None
     if a.sweep and world == 1 and rank == 0:
         sweep = batch_sweep(a, ix, dev, nloc, D, k)
+    large_k = None
+    if a.large_k and world == 1 and rank == 0:
+        large_k = large_k_leg(ix, dev, nloc, D, ks=[int(x) for x in a.large_k.split(",") if x])
     c1 = c4 = None
     if rank == 0 and world == 1 and not a.no_configs1:
         c1 = configs1_leg(a, hc, dev)
@@ -775,7 +958,7 @@ def main():
                       "mfma_frac": round(flops / (avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
                       "hbm_frac_kernel": round(bytes_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "pipeline_ms_per_step": round(elapsed / a.steps * 1e3, 3),
-                      "batch_sweep": sweep},
+                      "batch_sweep": sweep, "large_k": large_k},
         }
     ix.close()
     if rank == 0 and world == 1 and not a.no_configs4:

@@ -29,7 +29,7 @@ using namespace hcr;
 
 #define set_err hcr_set_errorf     // errors.cpp: thread-local message + status code
 
-extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.2.0 (gfx950)"; }
+extern "C" const char* hcr_version(void) { return "hcrag-mi355x 0.3.0 (gfx950)"; }
 extern "C" int hcr_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -63,7 +63,6 @@ struct hcr_index {
       f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
-  int opt_qw1_shape = 0;        // HCR_OPT_QW1_SHAPE
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
   int opt_qs = 0;               // HCR_OPT_QS_FORM (0: the heuristic)
   int opt_prepass = 0;          // HCR_OPT_PREPASS (0: the heuristic)
@@ -413,12 +412,8 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   switch (option) {
     case HCR_OPT_QW1:
-      if (value < -1 || value > 5) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 5]", value);
+      if (value < -1 || value > 1) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 1]", value);
       ix->opt_qw1 = value;
-      return HCR_OK;
-    case HCR_OPT_QW1_SHAPE:
-      if (value < 0 || value > 3) return set_err(HCR_EINVAL, "HCR_OPT_QW1_SHAPE value %d not in [0, 3]", value);
-      ix->opt_qw1_shape = value;
       return HCR_OK;
     case HCR_OPT_SAMPLE_STRIDE:
       if (value != 0 && (value < 2 || value > 4096))
@@ -430,7 +425,8 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       ix->opt_prepass = value;
       return HCR_OK;
     case HCR_OPT_QS_FORM:
-      if (value < 0 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not in [0, 4]", value);
+      if (value != 0 && value != 1 && value != 3)
+        return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not 0, 1 or 3", value);
       ix->opt_qs = value;
       return HCR_OK;
     default:
@@ -511,7 +507,7 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_Q64_ELEMS")) t.q64_elems = (int64_t)atoll(e);
     if (const char* e = getenv("HCRAG_QS_MAX")) t.qs_max = atoi(e);
     if (const char* e = getenv("HCRAG_QW_MIN")) t.qw_min = std::max(1, atoi(e));
-    if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(5, std::max(-1, atoi(e)));
+    if (const char* e = getenv("HCRAG_QW1")) t.qw1 = std::min(1, std::max(-1, atoi(e)));
     t.no_prepass = getenv("HCRAG_NO_PREPASS") != nullptr;
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
@@ -527,13 +523,12 @@ static const TestHooks& hooks() {
 }
 
 // qs: query-stationary kernel (score_qs.h); qw: its 256-query form (score_qw.h); qw1: the
-// one-wave-per-SIMD form (score_qw1.h), spread = its DMA issue spread over the MFMA groups
-struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false, spread = false, nw8 = false, pipe = false,
-               qs4 = false; int hs = 2; };
+// one-wave-per-SIMD form at D = 1024 (score_qw1.h)
+struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false; int hs = 2; };
 // qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
-// QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1
+// QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1; opt_qs: HCR_OPT_QS_FORM
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1,
-                    int qw1_shape = 0, int opt_qs = 0) {
+                    int opt_qs = 0) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
@@ -541,17 +536,11 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   // B = 256 3.73 vs 4.61); at D = 384 QS and QW tie at 129-256 (1M x 384, B = 256: 0.283 vs
   // 0.282 ms), so QW from 257 there.
   const int qw_from = hooks().qw_min > 0 ? hooks().qw_min : (ld / V3_BK >= 24 ? 129 : 257);
-  // QW1: 64 (D = 768) / 48 (D = 1024) queries per wave at one wave per SIMD.  D = 1024 has no
-  // other query-stationary kernel (256 queries x 1024 do not fit QW's waves), so it takes QW1
-  // from 257 queries by default; D = 768 only when asked (HCR_OPT_QW1).
-  if (opt_qw1 != 0 && unit_ok && qw1_ok && qw1_supported(ld)) {
-    const bool d1024 = ld / V3_BK == 32;
-    const bool nw8 = (opt_qw1 == 3 || opt_qw1 == 4) && qw1_nw8_supported(ld);   // 8-wave form (D = 384)
-    const bool pipe = opt_qw1 == 5;                                 // QW1P (score_qw1p.h)
-    if ((opt_qw1 > 0 || d1024) && nq >= (d1024 ? 257 : ld / V3_BK == 12 ? 129 : qw_from))
-      return {qw1_rows(ld, pipe ? kQw1Pipelined : qw1_shape), qw1_queries(ld), 0, false, false, true,
-              opt_qw1 != 2 && opt_qw1 != 4, nw8, pipe};
-  }
+  // QW1: 48 queries per wave at one wave per SIMD, D = 1024 only.  D = 1024 has no other
+  // query-stationary kernel (256 queries x 1024 do not fit QW's waves), so it takes QW1 from 257
+  // queries unless HCR_OPT_QW1 = 0 (v4 then).
+  if (opt_qw1 != 0 && unit_ok && qw1_ok && qw1_supported(ld) && nq >= 257)
+    return {qw1_rows(ld), qw1_queries(ld), 0, false, false, true};
   if (nq >= qw_from && unit_ok && qw_ok && qw_supported(ld))
     return {qw_rows(ld), kQwQueries, kQwStages, false, true};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
@@ -559,23 +548,15 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
   // vs 4.45, B = 256 4.52 vs 4.59; 1M x 384 B = 32 0.187 vs 0.295, B = 256 0.290 vs 0.331.
   if (nq <= hooks().qs_max) {
-    // QS4 (HCR_OPT_QS_FORM = 2): 128-query 4-wave workgroups, two per CU (score_qs.h).  Not the
-    // default: r03 A/B at 1M x 384, B = 256 (score ms, two boxes): 0.2688 vs 0.2702 (8-wave) at
-    // stride 64, 0.2637 vs 0.2701 at 32; 0.2763 vs 0.2683 at 64, and the 8-wave form at 16 0.262.
-    if (opt_qs == 2 && nq > 64 && qs_supported(ld, 2)) {
-      V3Cfg c{128, 128, 4, true};
-      c.qs4 = true;
-      return c;
-    }
     // 129-256 queries with KS <= 12: one 256-query block on 128-row tiles (each row filled
     // into LDS once instead of once per 128-query block)
     if (nq > 128 && qs_supported(ld, 2)) {
       V3Cfg c{128, 256, 8, true};
       // KS = 12 (D = 384, configs[1]): 128-deep ring stages by default -- 3 barriers per 128-row
       // tile instead of 6 (r03 A/B, 1M x 384, B = 256, score ms: 64-deep 0.2694, 128-deep
-      // 0.2536, 192-deep 0.2559; stamps: 14.1k -> 12.2k cycles per tile); HCR_OPT_QS_FORM 1 / 4:
-      // 64- / 192-deep
-      if (ld / V3_BK == 12 && opt_qs != 1) c.hs = opt_qs == 4 ? 6 : 4;
+      // 0.2536, 192-deep 0.2559; stamps: 14.1k -> 12.2k cycles per tile); HCR_OPT_QS_FORM 1:
+      // 64-deep
+      if (ld / V3_BK == 12 && opt_qs != 1) c.hs = 4;
       return c;
     }
     // (KS = 24 without the UNIT epilogue spills VGPRs in its tile loop: v3/v4 then)
@@ -633,17 +614,15 @@ static int launch_qs_ix(hcr_index* ix, V3Cfg c, V3Launch a, hipStream_t st) {
            ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr, ix->w_qhat.p, a.nqb, a.P,
            a.nvt, a.tstride, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, qs_cap(a.kp), a.unit,
-           (c.qt == 256 || c.qs4) ? 2 : 1, c.qs4 ? 4 : 8, c.hs};
+           c.qt == 256 ? 2 : 1, c.hs};
   return launch_qs(ix->dtype, q, st);
 }
 
-static int launch_qw1_ix(hcr_index* ix, V3Launch a, int cap, bool spread, bool nw8, bool pipe,
-                         hipStream_t st) {
+static int launch_qw1_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
   QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
            a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
-           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true,
-           pipe ? kQw1Pipelined : ix->opt_qw1_shape};
-  return launch_qw1(ix->dtype, q, spread, nw8, st);
+           ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
+  return launch_qw1(ix->dtype, q, st);
 }
 
 // Row partitions of a QW1 launch (one workgroup per CU, LDS-bound): the smallest P >= 256 / nqb
@@ -721,7 +700,7 @@ template <typename TM>
 static int dispatch_v3(hcr_index* ix, V3Cfg c, V3Launch a, int cap, hipStream_t st) {
   if (c.qs) return launch_qs_ix(ix, c, a, st);              // CAP chosen in score_qs.hip
   if (c.qw) return launch_qw_ix(ix, a, cap, st);
-  if (c.qw1) return launch_qw1_ix(ix, a, cap, c.spread, c.nw8, c.pipe, st);
+  if (c.qw1) return launch_qw1_ix(ix, a, cap, st);
   switch (cap) {
     case 512: return launch_v3_cap<TM, 512>(ix, c, a, st);
     case 1024: return launch_v3_cap<TM, 1024>(ix, c, a, st);
@@ -959,7 +938,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
                           qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
-                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qw1_shape, ix->opt_qs);
+                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qs);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   if (hooks().debug_cfg)
     fprintf(stderr, "[hcrag] search_pass nq=%d n=%lld ld=%d kp=%d unit_dev=%.3g rho=%.3g mask=%d "
@@ -975,15 +954,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
   const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : qw1 ? qw1_cap(kp, ix->ld) : next_pow2(kp + tr);
-  // (QS4: two 4-wave workgroups per CU)
-  const int wg_target = (ver == 1 || (ver == 3 && c3.qs4)) ? 512 : 256;
+  const int wg_target = ver == 1 ? 512 : 256;
   // (QW: one workgroup per CU -- its LDS -- so at most 256 workgroups: one round)
   int P = qw1 ? qw1_partitions(nqb, ntiles)
                : qw ? std::max(1, wg_target / nqb) : std::max(1, (wg_target + nqb - 1) / nqb);
   P = std::min(P, ntiles);
   const int nwg = nqb * P;
-  // final lists per (query, partition): the 8-wave QW1 writes one per row half
-  const int PL = P * (qw1 && c3.nw8 ? 2 : 1);
+  const int PL = P;                     // final lists per query: one per partition
   const bool tm_f16 = ix->dtype == HCR_F16;
   const size_t tms = 2;
 
@@ -991,7 +968,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(ix->w_qnorm.ensure((size_t)nqpad * 8));
   CHECK(ix->w_eps.ensure((size_t)nqpad * 8));
   CHECK(ix->w_taug.ensure((size_t)nqpad * 4));
-  CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8 * (PL / P)));
+  CHECK(ix->w_buf.ensure((size_t)nwg * tq * cap * 8));
   CHECK(ix->w_part.ensure((size_t)nqpad * PL * kp * 8));
   CHECK(ix->w_pcnt.ensure((size_t)nqpad * PL * 4));
   CHECK(ix->w_merged.ensure(merge_workspace_keys(nqpad, PL, kp) * 8));
@@ -1014,8 +991,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const double unit_dev = unit ? ix->unit_dev_host : -1.0;
   ix->stats.unit_kernel = unit ? 1 : 0;
   if (ix->stats.score_kernel == 0)
-    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? (c3.pipe ? 9 : c3.nw8 ? 8 : 7) : qw ? 6
-                           : qs ? (c3.qs4 ? 10 : 5) : wide ? 4 : 3;
+    ix->stats.score_kernel = ver == 1 ? 1 : qw1 ? 7 : qw ? 6 : qs ? 5 : wide ? 4 : 3;
 
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   if (tm_f16)

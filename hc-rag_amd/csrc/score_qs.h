@@ -98,8 +98,11 @@ __device__ __forceinline__ void qs_read_u32x8(uint32_t a, uint32_t (&w)[8]) {
   w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 }
 
-template <int NST, int KS, int RT_, int NQ, int NW = 8, int HS = 2>
+constexpr int QS_NW = 8;         // waves per workgroup (two per SIMD)
+
+template <int NST, int KS, int RT_, int NQ, int HS = 2>
 struct QsLayout {
+  static constexpr int NW = QS_NW;
   static constexpr int RT = RT_, QT = 16 * NQ * NW;
   static constexpr int SPT = KS / HS;                      // stages per tile (32 HS-deep stages)
   static constexpr int STAGE = RT * 64 * HS;               // RT rows x 32 HS k: HS 32-deep halves
@@ -124,26 +127,20 @@ struct QsLayout {
 // KS <= 24 -- or (2, 128) -- 256 queries per workgroup for KS <= 12 (2 x KS x 4 VGPRs of query
 // fragments): every row is filled into LDS once per 256 queries instead of once per 128.
 //
-// NW = 4 ("QS4"): 4 waves (one per SIMD) and a 4 x 16 KiB ring -- ~68 KiB of LDS, so two
-// workgroups share a CU, each with its own barrier: the 8-wave form keeps every wave of the CU
-// in lock step (one barrier per stage, every wave's tile epilogue at the same time: the MFMA
-// pipe idles through epilogues and barrier skew, ~half of each tile at configs[1]); two
-// independent 4-wave workgroups drift apart, so one's epilogue runs under the other's MFMAs.
-// Rows are then filled into LDS once per 128 queries (the second query block's workgroup
-// reads them from the XCD's L2: consecutive workgroups of one XCD).
-//
-// HS: 32-deep k-steps per stage (2: 64-deep stages; 4 / 6 at configs[1]'s KS = 12: fewer
-// barriers per tile -- 3 or 2 instead of 6 -- each amortising the skew between the SIMD's two
-// waves and the fragment-read start-up over more MFMAs).
+// HS: 32-deep k-steps per stage (2: 64-deep stages; 4 at configs[1]'s KS = 12: 3 barriers per
+// tile instead of 6, each amortising the skew between the SIMD's two waves and the
+// fragment-read start-up over more MFMAs).  (r03 also built a 4-wave two-workgroups-per-CU form,
+// QS4, and 192-deep stages; neither measured faster -- profiles/r03/qs_forms/ -- removed in r04.)
 template <typename TM, int CAP, int KS, bool UNIT, int NQ = 1, int RT_ = 256,
-          int NST = (RT_ == 256 ? 4 : 8), int NW = 8, int HS = 2>
-__global__ void __launch_bounds__(NW * 64, 8 / NW)
+          int NST = (RT_ == 256 ? 4 : 8), int HS = 2>
+__global__ void __launch_bounds__(QS_NW * 64, 1)
 score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = QsLayout<NST, KS, RT_, NQ, NW, HS>;
+  using L = QsLayout<NST, KS, RT_, NQ, HS>;
+  constexpr int NW = QS_NW;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int RT = L::RT, QT = L::QT, MT = RT / 16, D = NST - 1, SPT = L::SPT;
@@ -437,14 +434,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
         const uint64_t key = make_key(sc, rowl);
         if (key > tkr[n]) {
-#ifndef HCR_QS_NOAPPEND   // (diagnostic stamps builds only: what the appends / their stores cost)
           const int ql = qlane + 16 * n;
           const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-#ifndef HCR_QS_NOSTORE
           wbuf[(size_t)ql * CAP + pos] = key;
-#endif
           need |= pos + 1 > CAP - RT;
-#endif
         }
       };
 #pragma unroll

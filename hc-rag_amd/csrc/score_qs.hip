@@ -12,37 +12,24 @@ using namespace hcr;
 
 namespace {
 
-template <typename TM, int CAP, int KS, int NQ, int RT, int NST = (RT == 256 ? 4 : 8), int NW = 8,
-          int HS = 2>
+template <typename TM, int CAP, int KS, int NQ, int RT, int NST = (RT == 256 ? 4 : 8), int HS = 2>
 void launch_t(const QsArgs& a, hipStream_t st) {
   if (a.unit)
-    hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, true, NQ, RT, NST, NW, HS>), dim3(a.nqb * a.P),
-                       dim3(NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
+    hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, true, NQ, RT, NST, HS>), dim3(a.nqb * a.P),
+                       dim3(QS_NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
                        a.mask, static_cast<const TM*>(a.qhat), a.nqb, a.P, a.ntiles, a.tstride,
                        a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
   else
-    hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, false, NQ, RT, NST, NW, HS>), dim3(a.nqb * a.P),
-                       dim3(NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
+    hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, false, NQ, RT, NST, HS>), dim3(a.nqb * a.P),
+                       dim3(QS_NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
                        a.mask, static_cast<const TM*>(a.qhat), a.nqb, a.P, a.ntiles, a.tstride,
                        a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP>
 bool by_ks(int ks, int nq_blocks, const QsArgs& a, hipStream_t st) {
-  if (nq_blocks == 2 && a.nw == 4) {   // QS4: 128 queries per 4-wave workgroup, 2 per CU
-    switch (ks) {
-      case 4: launch_t<TM, CAP, 4, 2, 128, 4, 4>(a, st); return true;
-      case 6: launch_t<TM, CAP, 6, 2, 128, 4, 4>(a, st); return true;
-      case 12: launch_t<TM, CAP, 12, 2, 128, 4, 4>(a, st); return true;
-      default: return false;
-    }
-  }
   if (nq_blocks == 2 && ks == 12 && a.hs == 4) {   // 128-deep stages, 4 x 32 KiB ring
-    launch_t<TM, CAP, 12, 2, 128, 4, 8, 4>(a, st);
-    return true;
-  }
-  if (nq_blocks == 2 && ks == 12 && a.hs == 6) {   // 192-deep stages, 3 x 48 KiB ring
-    launch_t<TM, CAP, 12, 2, 128, 3, 8, 6>(a, st);
+    launch_t<TM, CAP, 12, 2, 128, 4, 4>(a, st);
     return true;
   }
   if (nq_blocks == 2) {            // 256 queries per workgroup on 128-row tiles (KS <= 12)

@@ -18,19 +18,15 @@ struct QsArgs {
   int kp;
   int cap;                   // qs_cap(kp)
   bool unit;                 // raw dot products as coarse scores (L2-normalised corpus)
-  int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles);
-                             // QW1: its tuning shape (HCR_OPT_QW1_SHAPE)
-  int nw = 8;                // QS waves per workgroup: 8, or 4 with nq_blocks 2 (QS4: two
-                             // 128-query workgroups per CU)
-  int hs = 2;                // 32-deep k-steps per ring stage (2; 4 or 6 for the 8-wave
-                             // 256-query form at KS = 12)
+  int nq_blocks;             // 16-query blocks per wave: 1 (256-row tiles) or 2 (128-row tiles)
+  int hs = 2;                // 32-deep k-steps per ring stage (2; 4 for the 256-query form at
+                             // KS = 12)
   float* umax = nullptr;     // QW: the MAXONLY sampling pre-pass into umax[unit][nqb * 256]
                              // (ntiles = virtual stages of the sampled tiles, tstride their stride)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128
-// queries per workgroup on 256-row tiles; 2: 256 queries on 128-row tiles, or 128 per 4-wave
-// workgroup in the QS4 form).
+// queries per workgroup on 256-row tiles; 2: 256 queries on 128-row tiles).
 bool qs_supported(int ld, int nq_blocks);
 // Candidate buffer slots per query for k'.
 int qs_cap(int kp);
@@ -48,13 +44,10 @@ int launch_qw(int dtype, const QsArgs& a, hipStream_t st);
 constexpr int kQwQueries = 256;       // queries per QW workgroup (= QW_QT)
 constexpr int kQwStages = 3;          // QW ring stages (= QW_NST)
 
-// One-wave-per-SIMD query-stationary kernel (score_qw1.h): 256 (D = 768) or 192 (D = 1024)
-// queries per workgroup, UNIT corpora without a row mask.
+// One-wave-per-SIMD query-stationary kernel (score_qw1.h): D = 1024, 192 queries per workgroup,
+// UNIT corpora without a row mask.
 bool qw1_supported(int ld);
-int qw1_rows(int ld, int shape);      // rows per stage (the kernel's row tile) of a tuning shape
+int qw1_rows(int ld);                 // rows per stage (the kernel's row tile)
 int qw1_queries(int ld);              // queries per workgroup
 int qw1_cap(int kp, int ld);          // candidate buffer slots per query (0: k' too large)
-bool qw1_nw8_supported(int ld);       // the 8-wave form (two row halves per query set): D = 384
-constexpr int kQw1Pipelined = 4;      // QsArgs::nq_blocks / qw1_rows shape of QW1P (score_qw1p.h)
-// nw8: the 8-wave form, whose final lists are P x 2 per query (row half h of partition p: 2p + h)
-int launch_qw1(int dtype, const QsArgs& a, bool spread, bool nw8, hipStream_t st);
+int launch_qw1(int dtype, const QsArgs& a, hipStream_t st);

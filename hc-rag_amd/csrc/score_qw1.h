@@ -1,26 +1,21 @@
 // score_qw1.h — K2 "QW1": the wide query-stationary score + top-k' kernel at ONE wave per
-// SIMD, for large batches (MFMA-bound: configs[2] 10M x 768 B = 1024, configs[4] D = 1024).
+// SIMD, for large batches at D = 1024 (MFMA-bound: configs[4], bge-large 100M x 1024 bf16).
 //
-// Why.  QW (score_qw.h) runs two waves per SIMD with 32 queries each: every A (row) fragment
-// read from LDS feeds 2 MFMAs, so each wave reads the whole 48 KiB stage and the CU reads
-// 8 x the stage per stage (384 KiB).  The chip holds its clock down under this load (MI355X:
-// DVFS give-back), and LDS read bytes are part of the energy per MFMA.  QW1 gives each wave a
-// whole SIMD -- 512 registers -- and 4 (D = 768) or 3 (D = 1024) query blocks of 16: each A
-// fragment then feeds 8 or 6 MFMAs, the CU reads 4 x the stage, and D = 1024 (which does not fit
-// QW's 256-register waves) gets a query-stationary kernel too.
+// Why.  QW (score_qw.h) runs two waves per SIMD with 32 queries x the whole K each in 256
+// registers, which caps K at 768.  QW1 gives each wave a whole SIMD -- 512 registers -- and 3
+// query blocks of 16 at D = 1024: each A (row) fragment read from LDS feeds 6 MFMAs and the CU
+// reads 4 x the stage per stage.
 //
-//  * query fragments: QB x KS x 4 registers (384 at both shapes), the first 64 fragments in
+//  * query fragments: QB x KS x 4 = 384 registers, the first 64 fragments in
 //    AGPRs (an MFMA takes its A/B operands from either half of the unified file), the rest in
 //    VGPRs; loaded once by inline asm with "=a" / "=v" outputs so the compiler never copies them;
-//  * a stage is SR rows x the whole K (SR = 32: 48 KiB at D = 768; SR = 16: 32 KiB at D = 1024)
-//    in an NST-deep LDS-DMA ring (3 x 48 or 4 x 32 KiB), the v3 piece image (1 KiB pieces of 16
+//  * a stage is SR = 16 rows x the whole K (32 KiB) in a 4-deep LDS-DMA ring, the v3 piece image (1 KiB pieces of 16
 //    rows x 32 k, XOR-swizzled 16-byte chunks); each wave DMAs PIECES / 4 pieces + its 64 global
 //    bounds (a 4-byte-per-lane DMA) per stage;
 //  * fragment reads: one VGPR base per stage, every group's reads through the ds_read offset
 //    field (no per-group address arithmetic), FD groups in flight;
-//  * the DMA issue of stage s + NST - 1 is either all at the stage barrier or spread over the
-//    MFMA groups (template SPREAD: with no partner wave on the SIMD, an issue slot between MFMAs
-//    is the only place to hide it);
+//  * the DMA issue of stage s + NST - 1 is spread over the MFMA groups (with no partner wave on
+//    the SIMD, an issue slot between MFMAs is the only place to hide it);
 //  * the epilogue is QW's: per stage, the max of each query's SR scores against max(local k'-th
 //    key, global bound), appends into the wave's own candidate buffers, compaction when full,
 //    final lists at the end (topk_kernels.h).
@@ -56,40 +51,29 @@ __device__ __forceinline__ void static_for(F&& f) {
   }(std::make_integer_sequence<int, N>{});
 }
 
+// D = 1024 (configs[4], bge-large): 3 query blocks of 16 per wave, 16-row stages (32 KiB) in a
+// 4-deep ring.  (r03 also built D = 384 / 768 shapes, an 8-wave form and a software-pipelined
+// QW1P; none measured faster than QS / QW on those shapes -- profiles/r03/ab_c1_*, ab_c2_* --
+// and they were removed in r04.)
 template <int KS> struct Qw1Shape;
-template <> struct Qw1Shape<24> { static constexpr int QB = 4, SR = 32, NST = 3; };   // D = 768
-template <> struct Qw1Shape<32> { static constexpr int QB = 3, SR = 16, NST = 4; };   // D = 1024
-// D = 384 (configs[1]: HBM-bound at 256 queries): 24 KiB stages, 5 in flight
-template <> struct Qw1Shape<12> { static constexpr int QB = 4, SR = 32, NST = 6; };
+template <> struct Qw1Shape<32> { static constexpr int QB = 3, SR = 16, NST = 4; };
 
-// NW = 8 ("QW2", D = 384 only: 64 queries x 384 k = 192 registers, so two waves fit a SIMD):
-// waves w and w + 4 hold the same 64 queries and take the two row halves of every stage, each
-// with its own candidate buffers and final lists (row half h of partition p is list 2 p + h), so
-// the partner wave on the SIMD hides DMA issue, epilogues and barrier skew while each row
-// fragment is still read by only 4 waves.
-template <int KS, int NW = QW1_NW> struct Qw1Shape2 : Qw1Shape<KS> {};
-template <> struct Qw1Shape2<12, 8> { static constexpr int QB = 4, SR = 32, NST = 5; };
-
-template <int KS, int NW = QW1_NW, int QB = Qw1Shape2<KS, NW>::QB, int SR_ = Qw1Shape2<KS, NW>::SR,
-          int NST_ = Qw1Shape2<KS, NW>::NST>
+template <int KS, int QB = Qw1Shape<KS>::QB, int SR_ = Qw1Shape<KS>::SR, int NST_ = Qw1Shape<KS>::NST>
 struct Qw1Layout {
   static constexpr int SR = SR_, RB = SR / 16, NST = NST_;
-  static constexpr int H = NW / QW1_NW;                     // row halves (waves per query set)
-  static constexpr int RBW = RB / H;                        // row blocks per wave per stage
-  static constexpr int QPW = 16 * QB, QT = QW1_NW * QPW;  // queries per wave / workgroup
+  static constexpr int QPW = 16 * QB, QT = QW1_NW * QPW;    // queries per wave / workgroup
   static constexpr int PIECES = RB * KS;                    // 1 KiB pieces per stage
-  static constexpr int PPW = PIECES / NW;                   // ... per wave
+  static constexpr int PPW = PIECES / QW1_NW;               // ... per wave
   static constexpr int STAGE = PIECES * 1024;
   static constexpr int TGS = NST * STAGE;                   // [NST][NW waves][64 lanes] u32 bounds
-  static constexpr int TAU = TGS + NST * NW * 256;          // u64 tau_key[H][QT]
-  static constexpr int CNT = TAU + H * QT * 8;              // int cnt[H][QT]
-  static constexpr int TOTAL = CNT + H * QT * 4;
+  static constexpr int TAU = TGS + NST * QW1_NW * 256;      // u64 tau_key[QT]
+  static constexpr int CNT = TAU + QT * 8;                  // int cnt[QT]
+  static constexpr int TOTAL = CNT + QT * 4;
   static constexpr int NF = QB * KS;                        // query fragments per wave
-  // ... of them in AGPRs: 64 (256 registers) at one wave per SIMD; with two waves each wave's
-  // 256 registers split evenly (accum_offset 128), so 32
-  static constexpr int FA = NF < 64 / H ? NF : 64 / H;
+  // ... of them in AGPRs: 64 (256 registers) at one wave per SIMD
+  static constexpr int FA = NF < 64 ? NF : 64;
   static constexpr int FV = NF - FA;                        // ... in VGPRs
-  static_assert(SR > 0 && RBW >= 1 && (RBW == 1 || RBW % 2 == 0) && PIECES % NW == 0, "QW1 stage shape");
+  static_assert(SR > 0 && (RB == 1 || RB % 2 == 0) && PIECES % QW1_NW == 0, "QW1 stage shape");
   static_assert(QPW <= 64, "one 4-byte bound per lane");
   static_assert(STAGE <= 65536, "group offsets in the 16-bit ds_read offset field");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -131,27 +115,24 @@ __device__ __forceinline__ void qw1_issue_frags(uint32_t vbase, V (&av)[2]) {
                : "memory");
 }
 
-// SR_ / NST_ / FD_: overrides of the shape's stage rows, ring depth and fragment groups in flight
-// (0 = the shape's; tuning variants, HCR_OPT_QW1_SHAPE)
-template <typename TM, int CAP, int KS, bool SPREAD, int NW = QW1_NW, int SR_ = 0, int NST_ = 0,
-          int FD_ = 0>
-__global__ void __launch_bounds__(NW * 64, NW / QW1_NW)
+template <typename TM, int CAP, int KS>
+__global__ void __launch_bounds__(QW1_NW * 64, 1)
 score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                       const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                       uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                       uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
-  using L = Qw1Layout<KS, NW, Qw1Shape2<KS, NW>::QB, SR_ ? SR_ : Qw1Shape2<KS, NW>::SR,
-                      NST_ ? NST_ : Qw1Shape2<KS, NW>::NST>;
+  using L = Qw1Layout<KS>;
   using V = typename MfmaOp<TM>::V;
   using M = Qw1Mfma<TM>;
-  constexpr int SR = L::SR, RB = L::RBW, PPW = L::PPW, QT = L::QT, QPW = L::QPW, NST = L::NST;
-  constexpr int QB = QPW / 16, D = NST - 1, FA = L::FA, FV = L::FV, H = L::H;
+  constexpr int NW = QW1_NW;
+  constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = L::QT, QPW = L::QPW, NST = L::NST;
+  constexpr int QB = QPW / 16, D = NST - 1, FA = L::FA, FV = L::FV;
   constexpr int OPS = PPW + 1;                        // vmcnt-counted ops per wave per stage
   // fragment groups per stage (of the wave's RB row blocks): (row-block pair, k-step), or
   // (row block, k-step pair) if RB = 1
   constexpr int NG = RB == 1 ? KS / 2 : (RB / 2) * KS;
   constexpr int OFF2 = (RB == 1 ? 1 : KS) * 1024;
-  constexpr int FD = FD_ ? FD_ : H == 1 ? 3 : 2;      // fragment groups in flight (NW = 8: VGPRs)
+  constexpr int FD = 3;                               // fragment groups in flight
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -159,7 +140,6 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qset = wave & (QW1_NW - 1), half = wave / QW1_NW;   // query set, row half
 
   const int nwg = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -168,15 +148,12 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int t0 = (int)((int64_t)p * ntiles / P);
   const int t1 = (int)((int64_t)(p + 1) * ntiles / P);
   const int qbase = qb * QT;
-  uint64_t* wbuf = buf + ((size_t)b * H + half) * QT * CAP;
-  const int wq0 = qset * QPW;                         // this wave's first query (block-local)
-  tau_key += half * QT;                               // this row half's per-query state
-  cnt += half * QT;
-  const int PH = P * H, ph = p * H + half;            // this wave's final list: (query, ph)
+  uint64_t* wbuf = buf + (size_t)b * QT * CAP;
+  const int wq0 = wave * QPW;                         // this wave's first query (block-local)
 
   if (lane < QPW) { tau_key[wq0 + lane] = 0ull; cnt[wq0 + lane] = 0; }
   if (t0 >= t1) {
-    if (lane < QPW) pcnt[(size_t)(qbase + wq0 + lane) * PH + ph] = 0;
+    if (lane < QPW) pcnt[(size_t)(qbase + wq0 + lane) * P + p] = 0;
     return;
   }
 
@@ -260,18 +237,12 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #ifdef HCR_QW1_STAMPS
     HCR_QW1_STAMP(st_t1);
 #endif
-    const StageDesc nd = stage_desc(s + D);
-    if constexpr (!SPREAD) {
-#pragma unroll
-      for (int u = 0; u < OPS; ++u) issue_op(nd, u);
-    }
+    const StageDesc nd = stage_desc(s + D);   // issued spread over the MFMA groups below
 
     const int slot = s % NST;
     const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
-    // the wave's row half: its first row block's pieces (a wave-uniform offset of the stage)
-    const uint32_t sth = (uint32_t)__builtin_amdgcn_readfirstlane((int)(st + (uint32_t)(half * RB * KS * 1024)));
     uint32_t vbase;
-    asm volatile("v_add_u32 %0, %1, %2" : "=v"(vbase) : "s"(sth), "v"(offA));
+    asm volatile("v_add_u32 %0, %1, %2" : "=v"(vbase) : "s"(st), "v"(offA));
     // this stage's global bounds of the lane's QB queries: read now, waited for with the last
     // fragment group
     uint32_t tg[QB];
@@ -320,12 +291,12 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
         for (int n = 0; n < QB; ++n) asm volatile("" : "+v"(tg[n]));   // (read before: landed)
       }
-      if constexpr (SPREAD) {
-        static_for<OPS>([&](auto uc) {
-          constexpr int U = decltype(uc)::value;
-          if constexpr (U * NG / OPS == J) issue_op(nd, U);
-        });
-      }
+      // the next stage's DMA issue spread over the MFMA groups: with no partner wave on the
+      // SIMD, an issue slot between MFMAs is the only place to hide it
+      static_for<OPS>([&](auto uc) {
+        constexpr int U = decltype(uc)::value;
+        if constexpr (U * NG / OPS == J) issue_op(nd, U);
+      });
       if constexpr (RB == 1) {
         static_for<2>([&](auto kc) {
           constexpr int KK = decltype(kc)::value;
@@ -367,7 +338,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
     const int lq = le >> 4;
     const int qle = wq0 + (le & 15);                 // the query of accumulator block 0
-    const int64_t row0 = (int64_t)(t0 + s) * SR + half * RB * 16;   // the wave's first row
+    const int64_t row0 = (int64_t)(t0 + s) * SR;    // the tile's first row
     if (row0 + RB * 16 > n_rows) { // the corpus' last tile: rows past the end never pass (NaN)
 #pragma unroll
       for (int m = 0; m < RB; ++m)
@@ -408,9 +379,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                 if (key > tkr[n]) {
                   const int ql = qle + 16 * n;
                   const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-#ifndef HCR_QW1_NOSTORE   // (diagnostic stamps build only: what the appends' stores cost the ring)
                   wbuf[(size_t)ql * CAP + pos] = key;
-#endif
                   need |= pos + 1 > CAP - SR;
                 }
               }
@@ -451,7 +420,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + QPW, kp, lane, partials, pcnt, PH, ph);
+  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + QPW, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

@@ -15,7 +15,7 @@ from .ingest import BatchedEmbeddingGenerator, EmbeddingStore
 from . import relevance
 from . import graph_relevance
 
-__version__ = "0.2.0"
+__version__ = "0.3.0"
 
 __all__ = ["VectorIndex", "MultiDeviceIndex", "merge_topk_device", "EmbeddingSearch", "batch_semantic_similarity",
            "WordPieceTokenizer", "BertEncoder", "SentenceEmbedder", "MI355XEmbedding", "config_from_hf",

@@ -179,18 +179,16 @@ class VectorIndex:
         check(lib().hcr_index_set_timing(self._h, 1 if enable else 0))
 
     OPT_QW1 = 1
-    OPT_QW1_SHAPE = 2
     OPT_SAMPLE_STRIDE = 3
     OPT_QS_FORM = 4
     OPT_PREPASS = 5
 
     def set_option(self, option: int, value: int) -> None:
         """Kernel-choice option (``hcr_index_set_option``); never changes results.
-        ``VectorIndex.OPT_QW1``: -1 heuristic, 0 never QW1, 1 QW1 (DMA spread), 2 QW1 (DMA at
-        the stage barrier), 3 / 4 the same in the 8-wave form where it exists (D = 384).
+        ``VectorIndex.OPT_QW1``: D = 1024 from 257 queries: -1 / 1 QW1 (default), 0 never (v4).
         ``VectorIndex.OPT_SAMPLE_STRIDE``: the sampling pre-pass's row-tile stride (0 heuristic).
-        ``VectorIndex.OPT_QS_FORM``: 0 heuristic, 1 the 8-wave QS, 2 QS4 (D <= 384, 65-256 queries),
-        3 / 4 the 8-wave QS with 128- / 192-deep ring stages (D = 384, 129-256 queries).
+        ``VectorIndex.OPT_QS_FORM``: QS ring stages at D = 384, 129-256 queries: 0 heuristic,
+        1 64-deep, 3 128-deep.
         ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel under QW, 1 v4, 2 QW (0 heuristic)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 

@@ -146,10 +146,7 @@ typedef struct {
   int32_t score_kernel;       /* dense score kernel of the first pass: 1 register-staged
                                  128 x 128 (fp32 rows), 3 v3 (256 x 16 / 256 x 64), 4 v4
                                  (256 x 256), 5 query-stationary QS, 6 wide query-stationary QW,
-                                 7 QW1 (one wave per SIMD, 64 / 48 queries per wave),
-                                 8 QW1 in its 8-wave form (D = 384: two row halves per query set),
-                                 9 QW1P (QW1 software-pipelined, HCR_OPT_QW1 = 5),
-                                 10 QS4 (two 4-wave query-stationary workgroups per CU) */
+                                 7 QW1 (D = 1024: one wave per SIMD, 48 queries per wave) */
 } hcr_search_stats;
 int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 /* Enable (1) / disable (0) HIP-event timing of the fused score kernel (K2) on the stream it
@@ -157,28 +154,19 @@ int hcr_index_last_stats(const hcr_index* index, hcr_search_stats* out);
 int hcr_index_set_timing(hcr_index* index, int enable);
 
 /* Tuning options of one index (results never change, only which exact kernel computes them).
- *   HCR_OPT_QW1: large-batch kernel at D = 384 / 768 / 1024.  -1 = default heuristic, 0 = never
- *                QW1 (D = 384: QS, D = 768: QW, D = 1024: v4), 1 = QW1 with its DMA issue spread
- *                over the MFMA groups, 2 = QW1 with the DMA issue at the stage barrier, 3 / 4 = the
- *                same with the 8-wave form where it exists (D = 384), else as 1 / 2, 5 = QW1P (QW1
- *                software-pipelined: the previous stage's epilogue under the MFMAs).
- *   HCR_OPT_QW1_SHAPE: QW1's stage shape at D = 768 (tuning): 0 = 32-row stages, 3-deep ring,
- *                3 fragment groups in flight; 1 = 4 groups in flight; 2 = 16-row stages, 6-deep
- *                ring; 3 = both.
+ *   HCR_OPT_QW1: the large-batch kernel at D = 1024 (from 257 queries).  -1 / 1 = QW1 (the
+ *                default), 0 = never QW1 (v4).  No effect at other dimensions.
  *   HCR_OPT_SAMPLE_STRIDE: the sampling pre-pass reads every value-th row tile (0 = the
  *                heuristic: the largest power of two in [16, 128] leaving >= 150 sampled 256-row
  *                tiles; 2 .. 4096 otherwise).  A denser sample
  *                gives a tighter seed (fewer candidate appends in the dense pass) at the cost of
  *                a longer pre-pass.
- *   HCR_OPT_QS_FORM: the query-stationary kernel's form for 65-256 queries at D <= 384: 0 = the
- *                heuristic (= 3 at D = 384), 1 = one 8-wave workgroup per CU (256 queries on
- *                128-row tiles from 129 queries) with 64-deep ring stages, 2 = QS4 from 65
- *                queries (128-query 4-wave workgroups, two per CU), 3 / 4 = the 8-wave form with
- *                128- / 192-deep ring stages (D = 384 only, 129-256 queries).
+ *   HCR_OPT_QS_FORM: the query-stationary kernel's ring stages for 129-256 queries at D = 384:
+ *                0 = the heuristic (= 3), 1 = 64-deep stages, 3 = 128-deep stages.
  *   HCR_OPT_PREPASS: the sampling pre-pass kernel when the dense pass runs on QW: 0 = the
  *                heuristic, 1 = the 256 x 256 v4 kernel's MAXONLY form, 2 = QW's MAXONLY form. */
-typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_QW1_SHAPE = 2, HCR_OPT_SAMPLE_STRIDE = 3,
-               HCR_OPT_QS_FORM = 4, HCR_OPT_PREPASS = 5 } hcr_index_option;
+typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,
+               HCR_OPT_PREPASS = 5 } hcr_index_option;     /* (2: removed in 0.3) */
 int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)

@@ -2,8 +2,8 @@
 merge_lists_kernel + rescore_kernel launches (HCRAG_NO_FINISH, run in a child process): results
 must be bit-identical (same keys, same fp64 summation order), and both equal to the fp64 oracle.
 Shapes: configs[1]'s QS batch (P = 256 lists of k' = 64: one 16384-key level), a QW batch with
-a multi-level merge (k' = 512: G = 32 lists per level), and QW1's 8-wave form (two final lists
-per partition); all <= 512 queries (kFinishMaxQueries: larger batches take the separate
+a multi-level merge (k' = 512: G = 32 lists per level), and QW1 at D = 1024 (192-query blocks);
+all <= 512 queries (kFinishMaxQueries: larger batches take the separate
 launches).  Reference: experiments/main.py:841-844."""
 import os
 import subprocess
@@ -17,7 +17,7 @@ from oracle import cosine_topk as O
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = [(384, 150_000 + 77, 256, 10, -1), (768, 60_000 + 5, 512, 200, -1), (384, 80_000 + 1, 512, 32, 3)]
+CASES = [(384, 150_000 + 77, 256, 10, -1), (768, 60_000 + 5, 512, 200, -1), (1024, 40_000 + 1, 300, 32, -1)]
 
 _CHILD = r"""
 import sys, numpy as np
@@ -56,7 +56,7 @@ def _run(tmp_path, case, no_finish):
     return np.load(out)
 
 
-@pytest.mark.parametrize("case", CASES, ids=["qs_c1", "qw_k200", "qw1_nw8"])
+@pytest.mark.parametrize("case", CASES, ids=["qs_c1", "qw_k200", "qw1_d1024"])
 def test_finish_matches_separate_launches(tmp_path, case):
     a = _run(tmp_path, case, False)
     b = _run(tmp_path, case, True)

@@ -89,3 +89,15 @@ def test_configs2_full_size(env):
     B = 1024
     st = _run(env, 10_000_000, 768, B, 32, 1000, np.r_[0:4, B // 2:B // 2 + 4, B - 4:B])
     assert st["score_kernel"] in (6, 7), st
+
+
+def test_configs3_rank_full_size(env):
+    """configs[3] at its real per-rank size: a 1,250,000 x 768 f16 shard (10M
+    / 8), the 4096 gathered queries of --global-batch 4096, top-32 -- the QW route every rank of
+    the 8-GPU run takes; the queries on both sides of every 256-query block boundary checked
+    against the oracle over the whole shard."""
+    B = 4096
+    edges = np.arange(256, B, 256)
+    sub = np.unique(np.r_[0, edges - 1, edges, B - 1])
+    st = _run(env, 1_250_000, 768, B, 32, 1000, sub)
+    assert st["score_kernel"] == 6, st

@@ -1,11 +1,10 @@
-"""GPU parity of the query-stationary kernel's forms (HCR_OPT_QS_FORM): QS4 (score_qs.h with
-NW = 4: two 128-query 4-wave workgroups per CU, each with its own barrier; form 2) on the shapes
-it takes (D <= 384, 65-256 queries), and the 8-wave 256-query form with 128- / 192-deep ring
-stages (HS = 4 / 6; forms 3 / 4, D = 384, 129-256 queries): L2-normalised (UNIT epilogue) and
-raw corpora, a row mask, bf16.  Ids are compared
-EXACTLY with the fp64 oracle and scores to 1e-12; the stats must show that QS4 ran
-(score_kernel 10), so a silent reroute fails.  Reference: experiments/main.py:841-844
-(cosine_similarity + argsort[::-1][:k]) and :872-885 (the category filter)."""
+"""GPU parity of the query-stationary kernel's 256-query forms (score_qs.h, NQ = 2 on 128-row
+tiles, 129-256 queries): at D = 384 (KS = 12) with 64-deep (HCR_OPT_QS_FORM 1) and 128-deep
+(form 3, the default) ring stages, and at D = 128 / 192 (KS = 4 / 6: 64-deep) -- L2-normalised
+(UNIT epilogue) and raw corpora, a row mask, bf16.  Ids are compared EXACTLY with the fp64 oracle
+and scores to 1e-12; the stats must show that QS ran (score_kernel 5), so a silent reroute
+fails.  Reference: experiments/main.py:841-844 (cosine_similarity + argsort[::-1][:k]) and
+:872-885 (the category filter)."""
 import numpy as np
 import pytest
 
@@ -13,8 +12,7 @@ from oracle import cosine_topk as O
 
 pytestmark = pytest.mark.gpu
 
-QS4 = 10         # hcr_search_stats.score_kernel of QS4
-QS = 5           # ... of the 8-wave form (any stage depth)
+QS = 5           # hcr_search_stats.score_kernel of the query-stationary kernel
 
 
 @pytest.fixture(scope="module")
@@ -34,14 +32,12 @@ def _planted(rng, E, B, noise=0.2):
 
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("D,form", [(128, 2), (192, 2), (384, 2), (384, 3), (384, 4)])
-@pytest.mark.parametrize("B,k", [(65, 10), (200, 10), (256, 32)])
+@pytest.mark.parametrize("D,form", [(128, 0), (192, 0), (384, 1), (384, 3)])
+@pytest.mark.parametrize("B,k", [(200, 10), (256, 32)])
 @pytest.mark.parametrize("normalize", [True, False])
-def test_qs4_parity(hc, dtype, D, form, B, k, normalize):
+def test_qs_form_parity(hc, dtype, D, form, B, k, normalize):
     """N not a multiple of the 128-row tile, tens of tiles per workgroup (the seeded pre-pass
-    runs), a padded second query block (65, 200), the UNIT and the inverse-norm epilogues."""
-    if form != 2 and B <= 128:
-        pytest.skip("the deep-stage 8-wave forms take 129-256 queries")
+    runs), a padded second query block (200), the UNIT and the inverse-norm epilogues."""
     rng = np.random.default_rng(D * 7 + B + k + int(normalize) + form)
     N = 120000 + 77
     E = rng.standard_normal((N, D)).astype(np.float32)
@@ -54,7 +50,7 @@ def test_qs4_parity(hc, dtype, D, form, B, k, normalize):
         R = ix.get_rows()
         s, i = ix.search(Q, k)
         st = ix.last_stats()
-        assert st["score_kernel"] == (QS4 if form == 2 else QS), st
+        assert st["score_kernel"] == QS, st
         assert st["uncertified_queries"] == 0, st
     sub = np.r_[0:16, B // 2: B // 2 + 16, B - 8:B]
     es, ei = O.cosine_topk(Q[sub], R, k)
@@ -63,9 +59,9 @@ def test_qs4_parity(hc, dtype, D, form, B, k, normalize):
     np.testing.assert_array_equal(i[: B // 2, 0], src)
 
 
-def test_qs4_rowmask_and_default_form_agree(hc):
-    """A category mask (the mask words ride the tile-start DMA of wave NW-3), and QS4 vs the
-    8-wave form on the same index: identical ids and scores."""
+def test_qs_rowmask_and_forms_agree(hc):
+    """A category mask (the mask words ride the tile-start DMA of wave NW-3), and the 64- vs
+    128-deep forms on the same index: identical ids and scores."""
     rng = np.random.default_rng(11)
     N, D, B, k = 70000 + 3, 384, 256, 16
     E = rng.standard_normal((N, D)).astype(np.float32)
@@ -75,12 +71,14 @@ def test_qs4_rowmask_and_default_form_agree(hc):
         ix.add(E, normalize=True)
         ix.set_rowmask(mask)
         R = ix.get_rows()
-        ix.set_option(ix.OPT_QS_FORM, 2)
+        ix.set_option(ix.OPT_QS_FORM, 3)
         s4, i4 = ix.search(Q, k)
-        assert ix.last_stats()["score_kernel"] == QS4
+        assert ix.last_stats()["score_kernel"] == QS
         ix.set_option(ix.OPT_QS_FORM, 1)
         s8, i8 = ix.search(Q, k)
-        assert ix.last_stats()["score_kernel"] == 5
+        assert ix.last_stats()["score_kernel"] == QS
+        with pytest.raises(Exception):
+            ix.set_option(ix.OPT_QS_FORM, 2)          # QS4: removed
     np.testing.assert_array_equal(i4, i8)
     np.testing.assert_array_equal(s4, s8)
     es, ei = O.cosine_topk(Q[:24], R, k, rowmask=mask)

@@ -223,8 +223,10 @@ def test_device_api_and_shard_merge(hc):
 @pytest.mark.parametrize("W,B", [(2, 1024), (8, 1024), (8, 512)])
 def test_rank_shapes_of_the_scaling_bench(hc, W, B):
     """The local search each rank of ``bench.py --gpus W`` runs: nq = W x B gathered queries
-    (8192 at W = 8, B = 1024; 4096 = configs[3]'s global batch at W = 8, B = 512) over a row shard, through the same hip_local_search / hip_merge callables
-    ShardedSearch uses; the W shards run one after another on one GPU, the all-to-all is the
+    (8192 at W = 8, B = 1024; 4096 = configs[3]'s global batch at W = 8, B = 512) over a row
+    shard, through the same hip_local_search / hip_merge callables ShardedSearch uses (raw rows:
+    the non-UNIT v4 route; test_rank_route_of_configs3 below runs the bench's L2-normalised QW
+    route at full query counts); the W shards run one after another on one GPU, the all-to-all is the
     slice [j*B:(j+1)*B] of shard r's result, and the merged lists must equal the unsharded
     oracle exactly."""
     torch = pytest.importorskip("torch")
@@ -259,6 +261,40 @@ def test_rank_shapes_of_the_scaling_bench(hc, W, B):
     _check(got_s[sub], got_i[sub], es, ei, tol=SCORE_TOL_F64)
     # planted queries find their own row first
     assert np.mean(got_i[::2, 0] == planted) > 0.99
+
+
+@pytest.mark.parametrize("nq", [4096, 8192])
+def test_rank_route_of_configs3(hc, nq):
+    """configs[3]'s per-rank production route: a rank of ``bench.py --gpus 8
+    --global-batch 4096`` scores all 4096 gathered queries (8192 at --global-batch 8192) on an
+    L2-normalised 768-d f16 shard, which routes to QW (score_kernel 6) with 16 / 32 query blocks
+    over the row partitions.  >= 100k rows, a shard id offset, half the queries planted (a stored
+    row + noise, as bench.make_queries); the queries on both sides of every 256-query block
+    boundary are compared with the fp64 oracle (ids exactly, scores to 1e-12), and every planted
+    query must find its own row first.  Reference: experiments/main.py:841-844."""
+    torch = pytest.importorskip("torch")
+    from hcrag_amd.distributed import hip_local_search
+    rng = np.random.default_rng(nq)
+    D, N, k, off = 768, 131072 + 37, 32, 3 * 1_250_000
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    with hc.VectorIndex(D, "f16", capacity=N) as ix:
+        ix.add(E, normalize=True)
+        ix.set_id_offset(off)
+        R = ix.get_rows()
+        Q = rng.standard_normal((nq, D)).astype(np.float32)
+        planted = rng.integers(0, N, nq // 2)
+        Q[::2] = R[planted] + 0.05 * rng.standard_normal((nq // 2, D)).astype(np.float32) / D ** 0.5
+        s, i = hip_local_search(ix, k)(torch.from_numpy(Q).to("cuda:0"))
+        torch.cuda.synchronize()
+        st = ix.last_stats()
+        assert st["score_kernel"] == 6, st                 # QW, the bench's kernel at this shape
+        assert st["uncertified_queries"] == 0, st
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    np.testing.assert_array_equal(i[::2, 0], planted + off)
+    edges = np.arange(256, nq, 256)
+    sub = np.unique(np.r_[0, 1, edges - 1, edges, nq - 1])
+    es, ei = O.cosine_topk(Q[sub], R, k)
+    _check(s[sub], i[sub], es, np.where(ei >= 0, ei + off, -1), tol=SCORE_TOL_F64)
 
 
 def test_embedding_search_dropin(hc):

@@ -29,8 +29,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2",
-                    help="HCR_OPT_QW1 values, each optionally ':shape' (HCR_OPT_QW1_SHAPE) and "
-                         "':stride' (HCR_OPT_SAMPLE_STRIDE), e.g. -1:0:32")
+                    help="HCR_OPT_QW1 values, each optionally ':stride' (HCR_OPT_SAMPLE_STRIDE), "
+                         "':qs_form' and ':prepass', e.g. -1:32")
     a = ap.parse_args()
     import hcrag_amd as hc
     dev = torch.device("cuda", 0)
@@ -49,9 +49,8 @@ def main():
         ref = None
         for r in range(a.rounds):
             for vs in a.variants.split(","):
-                v, shape, stride, qsf, pre = (int(x) for x in (vs + ":0:0:0:0").split(":")[:5])
+                v, stride, qsf, pre = (int(x) for x in (vs + ":0:0:0").split(":")[:4])
                 ix.set_option(ix.OPT_QW1, v)
-                ix.set_option(ix.OPT_QW1_SHAPE, shape)
                 ix.set_option(ix.OPT_SAMPLE_STRIDE, stride)
                 ix.set_option(ix.OPT_QS_FORM, qsf)
                 ix.set_option(ix.OPT_PREPASS, pre)

@@ -21,12 +21,11 @@ from hcrag_amd import _lib  # noqa: E402
 
 N, D, B = (int(x) for x in sys.argv[1:4])
 opt = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-shape = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+shape = 0
 dev = torch.device("cuda:0")
 ix = hcrag_amd.VectorIndex(D, "f16", device=0, capacity=N)
 bench.make_shard(ix, hcrag_amd, 0, N, D, "f16", dev)
 ix.set_option(ix.OPT_QW1, opt)
-ix.set_option(ix.OPT_QW1_SHAPE, shape)
 Q = np.random.default_rng(1).standard_normal((B, D)).astype(np.float32)
 for _ in range(3):
     ix.search(Q, 32)
