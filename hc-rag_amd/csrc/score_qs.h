@@ -116,7 +116,9 @@ struct QsLayout {
   static constexpr int MSK = TG + NIS * TG_SLOT;           // NIS x 32 B of row-mask words
   static constexpr int TAU = MSK + NIS * 64;               // u64 tau_key[QT]
   static constexpr int CNT = TAU + QT * 8;                 // int cnt[QT]
-  static constexpr int TOTAL = CNT + QT * 4;
+  static constexpr int LS = 8;                             // staged append slots per query
+  static constexpr int SLOTS = CNT + QT * 4;               // u64 slots[QT][LS] (flush_staged)
+  static constexpr int TOTAL = SLOTS + QT * LS * 8;
   static_assert(KS % HS == 0, "whole stages per tile");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
@@ -436,7 +438,8 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         if (key > tkr[n]) {
           const int ql = qlane + 16 * n;
           const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-          wbuf[(size_t)ql * CAP + pos] = key;
+          if (pos < L::LS) v3_lds_store_u64(lds + L::SLOTS + (ql * L::LS + pos) * 8, key);
+          else wbuf[(size_t)ql * CAP + pos] = key;
           need |= pos + 1 > CAP - RT;
         }
       };
@@ -478,6 +481,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drain this wave's stores -- and, in order, its ring pieces -- only then)
       if (__any(need)) {
+        flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -507,6 +511,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
 
   // final: every query's surviving keys (at most k') appended to its region of the partials
+  flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 16 * NQ, kp, lane, partials, pcnt, P, p);
