@@ -1051,7 +1051,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
         // v4's form is LDS-fill-bound), on v4 otherwise; HCR_OPT_PREPASS 1 / 2 force v4 / QW
         if (qw && ix->opt_prepass != 1) {
           QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, nqb_pre,
-                   a.P, a.nvt * (256 / qw_rows(ix->ld)), a.tstride, ix->w_buf.as<uint64_t>(),
+                   a.P, a.nvt * (256 / qw_sample_rows(ix->ld)), a.tstride, ix->w_buf.as<uint64_t>(),
                    ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), kp, cap,
                    true, 0};
           q.umax = ix->w_umax.as<float>();

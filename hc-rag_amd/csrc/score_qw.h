@@ -48,7 +48,7 @@ struct QwLayout {
   static constexpr int TAU = TGS + NST * 8 * 256;         // u64 tau_key[QT]
   static constexpr int CNT = TAU + QW_QT * 8;             // int cnt[QT]
   static constexpr int TOTAL = CNT + QW_QT * 4;
-  static_assert(SR > 0 && (RB == 1 || RB % 2 == 0) && PIECES % 8 == 0, "QW stage shape");
+  static_assert(SR > 0 && SR % 16 == 0 && PIECES % 8 == 0, "QW stage shape");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
 };
 
@@ -104,9 +104,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   using V = typename Op::V;
   constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = L::NST, D = NST - 1;
   constexpr int OPS = PPW + 1;                       // vmcnt-counted ops per wave per stage
-  // fragment groups per stage: (row-block pair, k-step), or (row block, k-step pair) if RB = 1
-  constexpr int NG = RB == 1 ? KS / 2 : (RB / 2) * KS;
-  constexpr int OFF2 = RB == 1 ? 1 : KS;
+  // fragment groups per stage: (row-block pair, k-step) for the row-block pairs, then (the odd
+  // last row block, k-step pair) when RB is odd
+  constexpr int NGP = (RB / 2) * KS, NG = NGP + (RB % 2) * (KS / 2);
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -118,7 +118,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int nwg = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int qb = g % nqb, p = g / nqb;
+  // (wave-uniform values kept in SGPRs: derived in VGPRs by the integer divisions, they were
+  // spilled, and a reload after the stage barrier sat in the ring's vmcnt stream)
+  const int qb = __builtin_amdgcn_readfirstlane(g % nqb), p = __builtin_amdgcn_readfirstlane(g / nqb);
   constexpr int SPT8 = 256 / SR;                      // stages per sampled 256-row tile
   constexpr int SPU = 128 / SR;                       // stages per 128-row unit (MAXONLY)
   const int t0 = MAXONLY ? (int)((int64_t)p * (ntiles / SPU) / P) * SPU : (int)((int64_t)p * ntiles / P);
@@ -152,8 +154,6 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const int ldb = ld * 2;
   const int voff = drow * ldb + dchunk * 16;
   const char* rows_b = reinterpret_cast<const char*>(rows);
-  const __amdgpu_buffer_rsrc_t tg_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(tau_g + qbase), (short)0, QT * 4, 0x00020000);
 
   const int nsteps = t1 - t0;
   // Stage i (tile t0 + i) goes to ring slot i % NST: this wave's PPW row pieces (piece j =
@@ -176,7 +176,11 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   auto issue_op = [&](const StageDesc& d, int u) __attribute__((always_inline)) {
     if (u < PPW) {
       const int j = wave + 8 * u;
-      dma16(d.a, lds + d.slot * L::STAGE + j * 1024, voff, (j / KS) * 16 * ldb + (j % KS) * (V3_BK * 2));
+      // the piece's source offset re-derived per stage from an opaque copy of the row pitch:
+      // hoisted, the PPW offsets hold PPW SGPRs across the loop (48-row stages: SGPR spills)
+      int ldbs = ldb;
+      asm volatile("" : "+s"(ldbs));
+      dma16(d.a, lds + d.slot * L::STAGE + j * 1024, voff, (j / KS) * 16 * ldbs + (j % KS) * (V3_BK * 2));
     } else {
       // the lane offset re-derived here (opaque to the compiler: hoisted, it was spilled and
       // its reload waited for the ring)
@@ -228,17 +232,22 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
     for (int m = 0; m < RB; ++m) acc[m][0] = acc[m][1] = floatx4{0.f, 0.f, 0.f, 0.f};
     // group j: row blocks (2 (j / KS), +1) at k-step j % KS; FD groups of reads in flight
-    constexpr int FD = 3;
+    constexpr int FD = RB > 2 ? 2 : 3;              // (48-row stages: 8 more accumulator VGPRs)
     auto gbase = [&](int j) {
-      return st + (uint32_t)((RB == 1 ? 2 * j : 2 * (j / KS) * KS + j % KS) * 1024);
+      return st + (uint32_t)((j < NGP ? 2 * (j / KS) * KS + j % KS : (RB - 1) * KS + 2 * (j - NGP)) * 1024);
+    };
+    // (the second fragment of a group: the next row block, KS KiB on, or the next k-step)
+    auto issue = [&](int j, V (&dst)[2]) __attribute__((always_inline)) {
+      if (j < NGP) qw_issue_frags<KS, V>(gbase(j), offA, dst);
+      else qw_issue_frags<1, V>(gbase(j), offA, dst);
     };
     V av[FD][2];
 #pragma unroll
-    for (int j = 0; j < FD - 1; ++j) qw_issue_frags<OFF2, V>(gbase(j), offA, av[j]);
+    for (int j = 0; j < FD - 1; ++j) issue(j, av[j]);
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
       if (j + FD - 1 < NG) {
-        qw_issue_frags<OFF2, V>(gbase(j + FD - 1), offA, av[(j + FD - 1) % FD]);
+        issue(j + FD - 1, av[(j + FD - 1) % FD]);
         qw_frag_wait<2 * (FD - 1)>(av[j % FD]);
       } else if (j + 1 < NG) {
         qw_frag_wait<2>(av[j % FD]);
@@ -246,12 +255,13 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         qw_frag_wait<0>(av[j % FD]);
         asm volatile("" : "+v"(tg2[0]), "+v"(tg2[1]));   // (read before the fragments: landed)
       }
-      if constexpr (RB == 1) {
+      if (j >= NGP) {
+        const int i = j - NGP;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int n = 0; n < 2; ++n)
-            acc[0][n] = Op::run(av[j % FD][kk], qf[n][2 * j + kk], acc[0][n]);
+            acc[RB - 1][n] = Op::run(av[j % FD][kk], qf[n][2 * i + kk], acc[RB - 1][n]);
       } else {
         const int m0 = 2 * (j / KS), k0 = j % KS;
 #pragma unroll
@@ -268,7 +278,10 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const int lq = le >> 4;
     const int qle = wq0 + (le & 15);                 // the query of accumulator block 0
     const int64_t row0 = real_stage(t0 + s) * SR;
-    if (row0 + SR > n_rows) {      // the corpus' last tile: rows past the end never pass (NaN)
+    // the corpus' last tile: rows past the end never pass (NaN).  A 32-bit scalar test (rows per
+    // shard < 2^32): the 64-bit compare is a VALU op on a VGPR copy of n_rows, spilled at SR = 48
+    const uint32_t nr32 = (uint32_t)n_rows;
+    if (nr32 < (uint32_t)SR || (uint32_t)row0 > nr32 - (uint32_t)SR) {
 #pragma unroll
       for (int m = 0; m < RB; ++m)
 #pragma unroll

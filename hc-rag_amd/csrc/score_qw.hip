@@ -2,6 +2,8 @@
 // (score_qw.h), in a translation unit of its own (compiles in parallel with the others).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "hcrag.h"
 #include "host_common.h"
 #define HCR_TOPK_TEMPLATES_ONLY   // the shared non-template kernels live in hcrag_index.hip
@@ -14,7 +16,11 @@ namespace {
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
-  if (a.umax)       // the sampling pre-pass (MAXONLY)
+  if constexpr (256 % SR != 0) {   // (a dense-only stage shape: the pre-pass never asks for it)
+    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
+                       static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+  } else if (a.umax)       // the sampling pre-pass (MAXONLY)
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                        st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
                        a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, a.tstride, a.umax);
@@ -24,11 +30,25 @@ void launch_t(const QsArgs& a, hipStream_t st) {
                        a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
+// Dense-pass stage shape at D = 768 (HCRAG_QW_SR, read once; test / A-B hook): 32 rows (48 KiB)
+// in a 3-deep ring, or 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows instead of
+// per 32.  The MAXONLY pre-pass keeps 32-row stages (its units are 128 rows).
+int dense_sr(int ks) {
+  static const int sr = [] {
+    const char* e = getenv("HCRAG_QW_SR");
+    return e ? atoi(e) : 32;
+  }();
+  return ks == 24 && sr == 48 ? 48 : qw_sr(ks);
+}
+
 template <typename TM, int CAP>
 bool by_ks(int ks, const QsArgs& a, hipStream_t st) {
   switch (ks) {
     case 12: launch_t<TM, CAP, 12>(a, st); return true;
-    case 24: launch_t<TM, CAP, 24>(a, st); return true;
+    case 24:
+      if (!a.umax && dense_sr(24) == 48) launch_t<TM, CAP, 24, 48, 2>(a, st);
+      else launch_t<TM, CAP, 24>(a, st);
+      return true;
     default: return false;
   }
 }
@@ -43,8 +63,9 @@ bool by_cap(const QsArgs& a, hipStream_t st) {
 }  // namespace
 
 bool qw_supported(int ld) { return ld % V3_BK == 0 && qw_sr(ld / V3_BK) > 0; }
-int qw_rows(int ld) { return qw_sr(ld / V3_BK); }
-int qw_cap(int kp, int ld) { return kp + qw_sr(ld / V3_BK) <= 256 ? 256 : 0; }   // 0: not supported
+int qw_rows(int ld) { return dense_sr(ld / V3_BK); }
+int qw_sample_rows(int ld) { return qw_sr(ld / V3_BK); }
+int qw_cap(int kp, int ld) { return kp + dense_sr(ld / V3_BK) <= 256 ? 256 : 0; }   // 0: not supported
 
 int launch_qw(int dtype, const QsArgs& a, hipStream_t st) {
   const bool ok = dtype == HCR_F16 ? by_cap<_Float16>(a, st) : by_cap<__bf16>(a, st);
