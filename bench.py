@@ -613,9 +613,10 @@ def configs4_leg(a, hc, dev, steps=3):
 def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     """Query-embedding throughput of one compute mode: B query token sequences per rank
     (S = --enc-seq, ragged lengths) -> BERT forward -> pool -> L2; whole-job embeddings/s over
-    the max-over-ranks time.  Useful FLOPs per query = 2 * P_nonemb * S + 4 * L * S^2 * H
-    (SURVEY.md §8(d)); the reference-precision mode executes 3x the projection FLOPs on MFMA
-    (three split-f16 terms), reported as mfma_frac_executed."""
+    the max-over-ranks time.  Useful FLOPs per sequence = 2 * P_nonemb * len + 4 * L * len^2 * H
+    (SURVEY.md §8(d), at each sequence's own token count: the encoder packs the valid tokens);
+    the reference-precision mode executes 3x the projection FLOPs on MFMA (three split-f16
+    terms), reported as mfma_frac_executed."""
     cfg = ENC_SHAPES[a.encoder]
     enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=mode, device=dev.index)
     S = a.enc_seq
@@ -623,6 +624,7 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     ids = torch.randint(1000, cfg["vocab_size"], (B, S), generator=g, dtype=torch.int32)
     lens = torch.randint(S // 2, S + 1, (B,), generator=g)
     mask = (torch.arange(S)[None, :] < lens[:, None]).to(torch.int32)
+    lens = mask.sum(1).double()
     ids = (ids * mask).to(dev)
     mask = mask.to(dev)
     out = torch.empty((B, cfg["hidden"]), dtype=torch.float32, device=dev)
@@ -646,11 +648,16 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
         el = float(t.item())
     H, F, L = cfg["hidden"], cfg["intermediate"], cfg["layers"]
     p_nonemb = L * (4 * H * H + 2 * H * F)
+    # model flops of the batch: every sequence at its own length (the tokens the result depends
+    # on; the encoder packs them, pack_tokens_kernel) -- and, for comparison with rounds before
+    # the packing, the padded basis (every sequence at S)
+    flops_batch = float((2.0 * p_nonemb * lens + 4.0 * L * lens * lens * H).sum())
     flops_q = 2.0 * p_nonemb * S + 4.0 * L * S * S * H
     per_step = el / a.enc_steps
-    tf = B * flops_q / per_step / 1e12
+    tf = flops_batch / per_step / 1e12
+    tf_padded = B * flops_q / per_step / 1e12
     gemm_mult = 3.0 if mode == "f32" else 1.0
-    tf_exec = B * (gemm_mult * 2.0 * p_nonemb * S) / per_step / 1e12
+    tf_exec = gemm_mult * 2.0 * p_nonemb * float(lens.sum()) / per_step / 1e12
     norms = out.norm(dim=1)
     enc.close()
     return {"mode": mode,
@@ -661,7 +668,9 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
             "query_embeddings_per_s": round(world * B / per_step, 1),
             "ms_per_batch": round(per_step * 1e3, 3),
             "gpu_ms_per_batch": round(ev0.elapsed_time(ev1) / a.enc_steps, 3),
-            "flops_per_query": flops_q, "TFLOPs": round(tf, 2),
+            "tokens_valid": int(lens.sum()), "tokens_padded": B * S,
+            "flops_per_batch": flops_batch, "TFLOPs": round(tf, 2),
+            "TFLOPs_padded_basis": round(tf_padded, 2),
             "mfma_frac": round(tf / MFMA_PEAK_TFLOPS, 4),
             "mfma_frac_executed": round(tf_exec / MFMA_PEAK_TFLOPS, 4),
             "unit_norm_ok": bool(((norms - 1).abs() < 1e-3).all().item())}

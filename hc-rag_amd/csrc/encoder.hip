@@ -49,6 +49,7 @@ struct hcr_encoder {
   std::vector<EncLayer> layers;
   // workspace
   DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out;
+  DevBuf pk_off, pk_map, pk_ok, pk_tot;   // token packing (pack_tokens_kernel)
   size_t att_lds_limit = 64 * 1024;
 };
 
@@ -57,7 +58,8 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Test hooks (read once): HCRAG_GEMM_FT=256|192 forces the GEMM feature tile; HCRAG_LN_SCALAR
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false; };
+// HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -66,6 +68,7 @@ static const EncHooks& enc_hooks() {
     // reference-precision FFN1 GELU with the library erff instead of erf_as
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
+    t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
     return t;
   }();
   return h;
@@ -361,14 +364,14 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
 }
 
 template <typename TM, int DH, int KB>
-static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                                  hipStream_t st) {
   const size_t lds = attention_mfma_lds<TM, DH>(S);
   if (lds > 64 * 1024)
     HIPC(hipFuncSetAttribute((const void*)attention_mfma_kernel<TM, DH, KB>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipLaunchKernelGGL((attention_mfma_kernel<TM, DH, KB>), dim3((unsigned)(n * e->cfg.heads)),
-                     dim3(256), lds, st, e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden,
+                     dim3(256), lds, st, e->qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden,
                      e->cfg.heads, e->ctx.as<TM>());
   HIPC(hipGetLastError());
   return HCR_OK;
@@ -376,15 +379,15 @@ static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, int64_t 
 
 // Fast modes: MFMA attention for head dims 32 / 64 up to 512 keys, the scalar kernel otherwise.
 template <typename TM>
-static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+static int launch_attention(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                             hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
   const int Sp = (S + 31) & ~31;
   if ((dh == 32 || dh == 64) && Sp <= 512) {
-    if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, d_mask, n, S, st)
-                                   : launch_attention_mfma<TM, 32, 32>(e, d_mask, n, S, st);
-    return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, d_mask, n, S, st)
-                     : launch_attention_mfma<TM, 64, 32>(e, d_mask, n, S, st);
+    if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, d_mask, seq_off, n, S, st)
+                                   : launch_attention_mfma<TM, 32, 32>(e, d_mask, seq_off, n, S, st);
+    return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, d_mask, seq_off, n, S, st)
+                     : launch_attention_mfma<TM, 64, 32>(e, d_mask, seq_off, n, S, st);
   }
   const size_t lds = (size_t)(5 * S + 4 * dh) * 4 + (size_t)2 * S * dh * sizeof(TM);
   if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
@@ -392,13 +395,13 @@ static int launch_attention(hcr_encoder* e, const int32_t* d_mask, int64_t n, in
     HIPC(hipFuncSetAttribute((const void*)attention_kernel<TM>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                     e->qkv.as<const TM>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<TM>());
+                     e->qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<TM>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
 // Reference-precision mode: fp32 attention, K/V in LDS when the sequence fits.
-static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n, int S,
+static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                                 hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
   if (S <= 64 && (dh == 32 || dh == 64)) {      // short sequences: f32 MFMA tiles
@@ -407,7 +410,7 @@ static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n
     const unsigned grid = (unsigned)(n * e->cfg.heads);
 #define HCR_ATT_MFMA(DH_, NT_)                                                                    \
   hipLaunchKernelGGL((attention_f32_mfma_kernel<DH_, NT_>), dim3(grid), dim3(64), lds, st,        \
-                     e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads,            \
+                     e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads,            \
                      e->ctx.as<_Float16>())
     if (dh == 64) {
       switch (nt) { case 1: HCR_ATT_MFMA(64, 1); break; case 2: HCR_ATT_MFMA(64, 2); break;
@@ -427,10 +430,10 @@ static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, int64_t n
   if (lds > 64 * 1024) HIPC(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   if (kv_lds)
     hipLaunchKernelGGL((attention_f32_kernel<true>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                       e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+                       e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
   else
     hipLaunchKernelGGL((attention_f32_kernel<false>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                       e->qkv.as<const float>(), d_mask, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+                       e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -441,8 +444,38 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
   const auto& c = e->cfg;
   const int H = c.hidden, F = c.intermediate;
   const int w = SPLIT ? 3 : 1;                        // activation row width factor
-  const int64_t T = n * (int64_t)S, Tp = rup(T, 256);
+  int64_t T = n * (int64_t)S;
   if (T > (int64_t)1 << 30) return hcr_set_error(HCR_EINVAL, "batch too large");
+  // Token packing (pack_tokens_kernel): only the tokens the result depends on run through the
+  // layers.  The packed row count is read back once (one stream synchronisation per batch):
+  // every grid below is sized by it.
+  const int32_t* tok_map = nullptr;
+  const int32_t* seq_off = nullptr;
+  const int32_t* key_mask = d_mask;                   // per-row key bits: padded mask or packed
+  if (!enc_hooks().padded) {
+    CHECK(e->pk_off.ensure((size_t)(n + 1) * 4));
+    CHECK(e->pk_map.ensure((size_t)T * 4));
+    CHECK(e->pk_ok.ensure((size_t)T * 4));
+    CHECK(e->pk_tot.ensure(4));
+    hipLaunchKernelGGL(pack_tokens_kernel, dim3(1), dim3(1024), 0, st, d_mask, n, S, c.pooling == 1 ? 1 : 0,
+                       e->pk_off.as<int32_t>(), e->pk_map.as<int32_t>(), e->pk_ok.as<int32_t>(),
+                       e->pk_tot.as<int32_t>());
+    HIPC(hipGetLastError());
+    int32_t tot = 0;
+    HIPC(hipMemcpyAsync(&tot, e->pk_tot.p, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    T = tot;
+    tok_map = e->pk_map.as<const int32_t>();
+    seq_off = e->pk_off.as<const int32_t>();
+    key_mask = e->pk_ok.as<const int32_t>();
+  }
+  if (T == 0) {                  // no token reaches the output (mean pooling, every mask 0)
+    hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st, e->x.as<const float>(),
+                       key_mask, seq_off, S, H, c.pooling, c.normalize, d_out);
+    HIPC(hipGetLastError());
+    return HCR_OK;
+  }
+  const int64_t Tp = rup(T, 256);
   CHECK(e->x.ensure((size_t)Tp * H * 4));
   CHECK(e->y.ensure((size_t)Tp * H * 4));
   CHECK(e->xh.ensure((size_t)Tp * H * w * sizeof(TM)));
@@ -463,12 +496,12 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
                          e->x.as<float>(), e->xh.as<TM>());
   };
   if (ln4)
-    hipLaunchKernelGGL((embed_ln4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+    hipLaunchKernelGGL((embed_ln4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
                        e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
   else
-    hipLaunchKernelGGL((embed_ln_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, (int)T, S, H,
+    hipLaunchKernelGGL((embed_ln_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
                        e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
@@ -479,12 +512,12 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
       CHECK((launch_gemm_split<EPI_BIAS_F32>(L.wqkv.as<const _Float16>(), e->xh.as<const _Float16>(), H,
                                              3 * H, (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
                                              e->qkv.as<float>(), 3 * H, L.sqkv, st)));
-      CHECK(launch_attention_f32(e, d_mask, n, S, st));
+      CHECK(launch_attention_f32(e, key_mask, seq_off, n, S, st));
     } else {
       CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
                                        L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
                                        3 * H, L.sqkv, st)));
-      CHECK(launch_attention<TM>(e, d_mask, n, S, st));
+      CHECK(launch_attention<TM>(e, key_mask, seq_off, n, S, st));
     }
     if constexpr (SPLIT)
       CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo.as<const _Float16>(), e->ctx.as<const _Float16>(), H, H,
@@ -516,7 +549,7 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
     HIPC(hipGetLastError());
   }
   hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st,
-                     e->x.as<const float>(), d_mask, S, H, c.pooling, c.normalize, d_out);
+                     e->x.as<const float>(), key_mask, seq_off, S, H, c.pooling, c.normalize, d_out);
   HIPC(hipGetLastError());
   return HCR_OK;
 }

@@ -135,15 +135,16 @@ layernorm4_kernel(const float* __restrict__ y, int T_real, int H, const float* _
 
 template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
-embed_ln4_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
+embed_ln4_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ tok_map, int T_real, int S, int H,
                  const float* __restrict__ wemb, const float* __restrict__ pemb,
                  const float* __restrict__ temb, const float* __restrict__ g,
                  const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T_real) return;
-  const float4* w = reinterpret_cast<const float4*>(wemb + (size_t)ids[t] * H);
-  const float4* p = reinterpret_cast<const float4*>(pemb + (size_t)(t % S) * H);
+  const int o = tok_map ? tok_map[t] : t;        // packed row -> its padded token index
+  const float4* w = reinterpret_cast<const float4*>(wemb + (size_t)ids[o] * H);
+  const float4* p = reinterpret_cast<const float4*>(pemb + (size_t)(o % S) * H);
   const float4* ty = reinterpret_cast<const float4*>(temb);
   float4 v[4];
 #pragma unroll
@@ -163,15 +164,16 @@ embed_ln4_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
 
 template <typename TM, bool SPLIT>
 __global__ void __launch_bounds__(256)
-embed_ln_kernel(const int32_t* __restrict__ ids, int T_real, int S, int H,
+embed_ln_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ tok_map, int T_real, int S, int H,
                 const float* __restrict__ wemb, const float* __restrict__ pemb,
                 const float* __restrict__ temb, const float* __restrict__ g,
                 const float* __restrict__ b, float eps, float* __restrict__ x, TM* __restrict__ xh) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T_real) return;
-  const float* w = wemb + (size_t)ids[t] * H;
-  const float* p = pemb + (size_t)(t % S) * H;
+  const int o = tok_map ? tok_map[t] : t;
+  const float* w = wemb + (size_t)ids[o] * H;
+  const float* p = pemb + (size_t)(o % S) * H;
   ln_row<TM, SPLIT>([&](int d) { return (w[d] + temb[d]) + p[d]; }, H, g, b, eps, lane,
                     x + (size_t)t * H, xh + (size_t)t * H * act_width<SPLIT>());
 }
@@ -231,17 +233,21 @@ __device__ __forceinline__ float gelu_exact(float x) { return 0.5f * x * (1.f + 
 // -------------------------------------------------------------------------------------
 template <typename TM>
 __global__ void __launch_bounds__(256)
-attention_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, int S, int H,
-                 int heads, TM* __restrict__ ctx) {
+attention_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask,
+                 const int32_t* __restrict__ seq_off, int S_pad, int H, int heads, TM* __restrict__ ctx) {
   extern __shared__ __attribute__((aligned(16))) float att_sm[];
   const int dh = H / heads;
   const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  // sequence bidx's rows: padded (rows bidx S_pad .., key mask = attention_mask) or packed
+  // (seq_off, key mask = the packed rows' own mask bits: pack_tokens_kernel)
+  const size_t row0 = seq_off ? (size_t)seq_off[bidx] : (size_t)bidx * S_pad;
+  const int S = seq_off ? seq_off[bidx + 1] - seq_off[bidx] : S_pad;
+  if (S == 0) return;
   float* Mk = att_sm;                                   // [S] additive key mask
   float* Pw = Mk + S;                                   // [4 waves][S] probabilities
   float* Qs = Pw + 4 * S;                               // [4 waves][dh] current query rows
   TM* Ks = reinterpret_cast<TM*>(Qs + 4 * dh);          // [S][dh]
   TM* Vs = Ks + (size_t)S * dh;                         // [S][dh]
-  const size_t row0 = (size_t)bidx * S;
   const int ld3 = 3 * H;
   for (int i = threadIdx.x; i < S * dh; i += blockDim.x) {
     const int j = i / dh, d = i - j * dh;
@@ -298,19 +304,23 @@ attention_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, i
 // -------------------------------------------------------------------------------------
 template <typename TM, int DH, int KB>
 __global__ void __launch_bounds__(256)
-attention_mfma_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask, int S, int H,
-                      int heads, TM* __restrict__ ctx) {
+attention_mfma_kernel(const TM* __restrict__ qkv, const int32_t* __restrict__ mask,
+                      const int32_t* __restrict__ seq_off, int S_pad, int H, int heads, TM* __restrict__ ctx) {
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int KS = DH + 16;                 // K row stride (elements)
   extern __shared__ __attribute__((aligned(16))) char att_mfma_sm[];
+  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
+  // sequence bidx's rows: padded (rows bidx S_pad .., key mask = attention_mask) or packed
+  // (seq_off, key mask = the packed rows' own mask bits: pack_tokens_kernel)
+  const size_t row0 = seq_off ? (size_t)seq_off[bidx] : (size_t)bidx * S_pad;
+  const int S = seq_off ? seq_off[bidx + 1] - seq_off[bidx] : S_pad;
+  if (S == 0) return;
   const int Sp = (S + 31) & ~31;
   const int VS = Sp + 8;                      // Vt row stride (elements)
   TM* Ks = reinterpret_cast<TM*>(att_mfma_sm);
   TM* Vt = Ks + (size_t)Sp * KS;
   float* Mk = reinterpret_cast<float*>(att_mfma_sm + (((size_t)Sp * KS + (size_t)DH * VS) * sizeof(TM) + 15) / 16 * 16);
-  const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
-  const size_t row0 = (size_t)bidx * S;
   const int ld3 = 3 * H;
   for (int i = threadIdx.x; i < Sp * (DH / 8); i += blockDim.x) {
     const int j = i / (DH / 8), c8 = i - j * (DH / 8);
@@ -434,12 +444,17 @@ __host__ __device__ inline size_t attention_f32_lds(int S, int dh, bool kv_lds) 
 
 template <bool KV_LDS>
 __global__ void __launch_bounds__(256)
-attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
-                     int H, int heads, _Float16* __restrict__ ctx) {
+attention_f32_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask,
+                     const int32_t* __restrict__ seq_off, int S_pad, int H, int heads,
+                     _Float16* __restrict__ ctx) {
   extern __shared__ __attribute__((aligned(16))) float attf_sm[];
   const int dh = H / heads;
   const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
-  const size_t row0 = (size_t)bidx * S;
+  // sequence bidx's rows: padded (rows bidx S_pad .., key mask = attention_mask) or packed
+  // (seq_off, key mask = the packed rows' own mask bits: pack_tokens_kernel)
+  const size_t row0 = seq_off ? (size_t)seq_off[bidx] : (size_t)bidx * S_pad;
+  const int S = seq_off ? seq_off[bidx + 1] - seq_off[bidx] : S_pad;
+  if (S == 0) return;
   const int ld3 = 3 * H;
   float* Mk = attf_sm;                    // [S] additive key mask
   float* Pw = Mk + S;                     // [4 waves][S]
@@ -531,8 +546,9 @@ __host__ __device__ inline size_t attention_f32_mfma_lds(int nt, int dh) {
 }
 template <int DH, int NT>
 __global__ void __launch_bounds__(64)
-attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask, int S,
-                          int H, int heads, _Float16* __restrict__ ctx) {
+attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restrict__ mask,
+                          const int32_t* __restrict__ seq_off, int S_pad, int H, int heads,
+                          _Float16* __restrict__ ctx) {
   constexpr int S16 = 16 * NT, LP = S16 + 1, CU = DH / 16, JI = S16 / 4;
   static_assert(DH % 16 == 0 && DH / 4 <= 16 * 4, "head size");
   extern __shared__ __attribute__((aligned(16))) float attm_sm[];
@@ -540,7 +556,11 @@ attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restri
   float* mk = Ps + S16 * LP;
   const int lane = threadIdx.x, lr = lane & 15, lk = lane >> 4;
   const int bidx = blockIdx.x / heads, h = blockIdx.x % heads;
-  const size_t row0 = (size_t)bidx * S;
+  // sequence bidx's rows: padded (rows bidx S_pad .., key mask = attention_mask) or packed
+  // (seq_off, key mask = the packed rows' own mask bits: pack_tokens_kernel)
+  const size_t row0 = seq_off ? (size_t)seq_off[bidx] : (size_t)bidx * S_pad;
+  const int S = seq_off ? seq_off[bidx + 1] - seq_off[bidx] : S_pad;
+  if (S == 0) return;
   const int ld3 = 3 * H;
   const float* base = qkv + row0 * ld3 + (size_t)h * DH;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -646,17 +666,70 @@ attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restri
 }
 
 // -------------------------------------------------------------------------------------
+// Token packing ("unpadding"): the tokens whose attention-mask bit is 1 -- plus position 0 of
+// every sequence when the pooling reads it (CLS; kept as a query row, a key only if its mask bit
+// is 1) -- stored contiguously, sequence after sequence in position order, so the projections,
+// FFN, LayerNorms and attention spend nothing on padding.  Row-wise kernels produce the same
+// values for a token either way; attention over the packed keys of a sequence is the padded
+// attention with its -inf keys left out (exactly 0 weight there).  One block: seq_off[n + 1]
+// (exclusive prefix sums of the per-sequence counts), tok_map[t] = b S + p (the padded index of
+// packed row t), key_ok[t] = that token's mask bit, total[0] = the packed row count.
+// -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+pack_tokens_kernel(const int32_t* __restrict__ mask, int64_t n, int S, int keep0,
+                   int32_t* __restrict__ seq_off, int32_t* __restrict__ tok_map,
+                   int32_t* __restrict__ key_ok, int32_t* __restrict__ total) {
+  __shared__ int32_t sc[1024];
+  int carry = 0;
+  for (int64_t b0 = 0; b0 < n; b0 += 1024) {
+    const int64_t b = b0 + threadIdx.x;
+    int c = 0;
+    if (b < n)
+      for (int p = 0; p < S; ++p) c += (mask[b * S + p] != 0 || (keep0 && p == 0)) ? 1 : 0;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {            // inclusive scan of the block's counts
+      const int v = threadIdx.x >= (unsigned)o ? sc[threadIdx.x - o] : 0;
+      __syncthreads();
+      sc[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (b < n) {
+      int t = carry + sc[threadIdx.x] - c;
+      seq_off[b] = t;
+      for (int p = 0; p < S; ++p) {
+        const int m = mask[b * S + p] != 0;
+        if (m || (keep0 && p == 0)) {
+          tok_map[t] = (int32_t)(b * S + p);
+          key_ok[t] = m;
+          ++t;
+        }
+      }
+    }
+    carry += sc[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    seq_off[n] = carry;
+    total[0] = carry;
+  }
+}
+
+// -------------------------------------------------------------------------------------
 // Pooling + L2 normalise (one block per sequence).
 //   mode 0 (sentence-transformers Pooling mean): sum_t h_t m_t / max(sum_t m_t, 1e-9)
 //   mode 1 (CLS, bge): h_0
 //   normalise: x / max(||x||, 1e-12)  (torch.nn.functional.normalize)
 // -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
-pool_normalize_kernel(const float* __restrict__ x, const int32_t* __restrict__ mask, int S,
-                      int H, int mode, int normalize, float* __restrict__ out) {
+pool_normalize_kernel(const float* __restrict__ x, const int32_t* __restrict__ mask,
+                      const int32_t* __restrict__ seq_off, int S_pad, int H, int mode, int normalize,
+                      float* __restrict__ out) {
   __shared__ float red[256];
   const int bidx = blockIdx.x;
-  const size_t row0 = (size_t)bidx * S;
+  // (packed rows: mask = the rows' own mask bits; a CLS sequence always holds its row 0)
+  const size_t row0 = seq_off ? (size_t)seq_off[bidx] : (size_t)bidx * S_pad;
+  const int S = seq_off ? seq_off[bidx + 1] - seq_off[bidx] : S_pad;
   float cnt = 0.f;
   if (mode == 0)
     for (int t = 0; t < S; ++t) cnt += (float)mask[row0 + t];

@@ -328,3 +328,68 @@ def test_ws_gemm_matches_v4(tmp_path):
         np.testing.assert_allclose(a, b, rtol=0, atol=5e-4, err_msg=key)
         cos = (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
         assert cos.min() >= 0.99999, (key, cos.min())
+
+
+_PADDED_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+d = np.load(sys.argv[3])
+from hcrag_amd import BertEncoder
+import json
+cfg = json.loads(str(d["cfg"]))
+state = {k[3:]: d[k] for k in d.files if k.startswith("sd_")}
+enc = BertEncoder(cfg, state, dtype=str(d["dtype"]))
+np.save(sys.argv[4], enc.encode_ids(d["ids"], d["mask"]))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,pool,shape", [("f32", "cls", "bge-base"), ("f32", "mean", "minilm"),
+                                              ("f16", "cls", "bge-base"), ("bf16", "mean", "tiny")])
+def test_packed_tokens_bit_identical_to_padded(tmp_path, dtype, pool, shape):
+    """Token packing (pack_tokens_kernel: only tokens with mask 1 -- plus a CLS row -- run through
+    the layers) against the padded path (HCRAG_ENC_PADDED=1, in a child process: the hook is read
+    once per process): with right padding every kept token sees the same keys in the same order
+    and every row-wise kernel computes the same row, so the embeddings are bit-identical."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from hcrag_amd import config_from_hf
+    cfg = {"bge-base": dict(BGE_BASE_2L, num_hidden_layers=3), "minilm": dict(MINILM, num_hidden_layers=2),
+           "tiny": TINY}[shape]
+    conf, m = _hf_model(cfg, 11)
+    rng = np.random.default_rng(11)
+    ids, mask = _batch(rng, 70, 32, cfg["vocab_size"])
+    hc_cfg = config_from_hf(conf.to_dict(), pool, True)
+    enc = _encoder(conf, m, dtype, pooling=pool)
+    got = enc.encode_ids(ids, mask)
+    inp = str(tmp_path / "in.npz")
+    np.savez(inp, ids=ids, mask=mask, dtype=dtype, cfg=json.dumps(hc_cfg),
+             **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "padded.npy")
+    subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, out],
+                   env=dict(os.environ, HCRAG_ENC_PADDED="1"), check=True, timeout=240)
+    np.testing.assert_array_equal(got, np.load(out))
+    _check(got, _ref_embed(m, ids, mask, pool), dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_packed_tokens_mask_holes_and_masked_cls(dtype):
+    """Masks that are not a prefix (holes, left padding) and a CLS-pooled sequence whose position
+    0 is masked out (BertModel still computes that query row; it is no key): the packed path
+    against fp32 BertModel, mean and CLS pooling."""
+    conf, m = _hf_model(TINY, 13)
+    rng = np.random.default_rng(13)
+    n, S = 12, 40
+    ids = rng.integers(5, TINY["vocab_size"], size=(n, S)).astype(np.int32)
+    mask = (rng.random((n, S)) < 0.7).astype(np.int32)
+    mask[0, :10] = 0                      # left padding
+    mask[1, 0] = 0                        # CLS row masked
+    mask[2, :] = 0
+    mask[2, 5] = 1                        # a single token, not at position 0
+    for pool in ("mean", "cls"):
+        enc = _encoder(conf, m, dtype, pooling=pool)
+        _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask, pool), dtype)
