@@ -315,6 +315,16 @@ extern "C" int hcr_index_add_ids(hcr_index* ix, const void* rows, int64_t n, int
 }
 
 extern "C" int64_t hcr_index_size(const hcr_index* ix) { return ix ? ix->n : -1; }
+
+int hcr_index_truncate_internal(hcr_index* ix, int64_t n) {
+  if (!ix || n < 0 || n > ix->n) return set_err(HCR_EINVAL, "bad truncation");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
+  HIPC(hipStreamSynchronize(ix->stream));
+  ix->n = n;
+  ix->rho_dirty = true;           // unit deviation re-measured over the rows that remain
+  return HCR_OK;
+}
 extern "C" int hcr_index_dim(const hcr_index* ix) { return ix ? ix->dim : -1; }
 extern "C" int hcr_index_dtype(const hcr_index* ix) { return ix ? ix->dtype : -1; }
 
@@ -452,6 +462,20 @@ static constexpr int kMaxDevices = 64;          // per-device once-only kernel a
 static constexpr size_t kLdsBytes = 160 * 1024;  // LDS per CU (gfx950) = a block's dynamic limit
 
 static int choose_kprime(int k) { return std::max(64, next_pow2(2 * k)); }
+
+// Raise a kernel's dynamic-LDS limit once per device (a per-device attribute; hcr_multi_search
+// runs shards of several devices concurrently).  `done` is the call site's own flag array: a
+// failure is returned to this caller and the next caller tries again (a once_flag
+// marked the attribute done even when setting it failed).
+static int raise_lds_limit(const void* fn, int bytes, int device, bool (&done)[kMaxDevices]) {
+  if (device < 0 || device >= kMaxDevices) return set_err(HCR_EINVAL, "device %d", device);
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done[device]) return HCR_OK;
+  HIPC(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done[device] = true;
+  return HCR_OK;
+}
 
 template <typename TS, typename TM, int CAP>
 static void launch_score(hcr_index* ix, int nqb, int P, int ntiles, int kp, hipStream_t st) {
@@ -731,13 +755,8 @@ template <typename TS>
 static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, int np, const float* d_q,
                          int nq, int kp, int k, int mode, double thr, double* out_s, int64_t* out_i,
                          hipStream_t st) {
-  static std::once_flag lds_once[kMaxDevices];
-  hipError_t lds_err = hipSuccess;
-  std::call_once(lds_once[ix->device], [&] {
-    lds_err = hipFuncSetAttribute((const void*)finish_kernel<TS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)kFinishDynLds);
-  });
-  HIPC(lds_err);
+  static bool lds_done[kMaxDevices];
+  CHECK(raise_lds_limit((const void*)finish_kernel<TS>, (int)kFinishDynLds, ix->device, lds_done));
   const int M = next_pow2(std::max(np * kp, kp));
   hipLaunchKernelGGL((finish_kernel<TS>), dim3(nq), dim3(256), finish_lds(np, kp, ix->dim), st, lists, cnt,
                      np, M, kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
@@ -849,14 +868,8 @@ static int merge_lists(hcr_index* ix, int nq, int nqpad, int P, int kp, hipStrea
                        const uint64_t** out, const int** out_cnt = nullptr, int* out_p = nullptr) {
   // the dynamic-LDS limit is a per-device attribute: raised once per device, by whichever
   // thread gets there first (hcr_multi_search runs shards of several devices concurrently)
-  static std::once_flag lds_once[kMaxDevices];
-  if (ix->device < 0 || ix->device >= kMaxDevices) return set_err(HCR_EINVAL, "device %d", ix->device);
-  hipError_t lds_err = hipSuccess;
-  std::call_once(lds_once[ix->device], [&] {
-    lds_err = hipFuncSetAttribute((const void*)merge_lists_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, kMergeMaxKeys * 8);
-  });
-  HIPC(lds_err);
+  static bool lds_done[kMaxDevices];
+  CHECK(raise_lds_limit((const void*)merge_lists_kernel, kMergeMaxKeys * 8, ix->device, lds_done));
   const int G = merge_groups(kp);
   const int P2 = (P + G - 1) / G;
   const uint64_t* src = ix->w_part.as<const uint64_t>();

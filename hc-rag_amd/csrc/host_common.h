@@ -9,6 +9,10 @@
 
 int hcr_set_error(int code, const char* msg);    // defined in hcrag_index.hip
 int hcr_set_errorf(int code, const char* fmt, ...);
+// Drop the rows past `n` of an index (multi.hip: rolls back a failed hcr_multi_add); internal,
+// not part of the C ABI.  Rows past the size are never scored; rho stays an upper bound.
+struct hcr_index;
+int hcr_index_truncate_internal(hcr_index* ix, int64_t n);
 
 #define HIPC(expr)                                                                          \
   do {                                                                                      \

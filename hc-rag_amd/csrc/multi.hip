@@ -18,6 +18,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -148,6 +149,8 @@ extern "C" int64_t hcr_multi_shard_size(const hcr_multi_index* m, int j) {
 extern "C" int hcr_multi_exchange_kind(const hcr_multi_index* m) { return m ? m->exchange : -1; }
 
 // n rows -> g contiguous blocks, block j appended to shard j with global ids m->n + offset.
+// All or nothing: when shard j's add fails, shards 0..j-1 drop the blocks they just took
+// (hcr_index_truncate_internal), so a failed call leaves the index as it was.
 extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, int rows_dtype,
                              int normalize) {
   if (!m) return hcr_set_error(HCR_EINVAL, "index is NULL");
@@ -157,6 +160,12 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
   if (rows_dtype != HCR_F16 && rows_dtype != HCR_BF16 && rows_dtype != HCR_F32)
     return hcr_set_errorf(HCR_EINVAL, "unknown rows dtype %d", rows_dtype);
   const size_t rb = (size_t)m->dim * (rows_dtype == HCR_F32 ? 4 : 2);
+  std::vector<int64_t> old_rows(m->g);
+  std::vector<size_t> old_gids(m->g);
+  for (int j = 0; j < m->g; ++j) {
+    old_rows[j] = hcr_index_size(m->sh[j].ix);
+    old_gids[j] = m->sh[j].gids.size();
+  }
   for (int j = 0; j < m->g; ++j) {
     const int64_t r0 = n * j / m->g, r1 = n * (j + 1) / m->g;
     if (r1 == r0) continue;
@@ -164,14 +173,23 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
     const size_t old = s.gids.size();
     s.gids.resize(old + (size_t)(r1 - r0));
     for (int64_t r = r0; r < r1; ++r) s.gids[old + (size_t)(r - r0)] = m->n + r;
-    const int rc = hcr_index_add_ids(s.ix, (const char*)rows + (size_t)r0 * rb, r1 - r0, rows_dtype,
-                                     normalize, s.gids.data() + old);
+    // (test hook HCRAG_FAIL_MULTI_ADD=j: shard j's add fails after its rows went in, as an
+    // allocation failure part-way through would -- tests/test_exact_gpu.py)
+    static const int fail_shard = [] {
+      const char* e = getenv("HCRAG_FAIL_MULTI_ADD");
+      return e ? atoi(e) : -1;
+    }();
+    int rc = hcr_index_add_ids(s.ix, (const char*)rows + (size_t)r0 * rb, r1 - r0, rows_dtype,
+                               normalize, s.gids.data() + old);
+    if (rc == HCR_OK && j == fail_shard) rc = hcr_set_error(HCR_EHIP, "injected failure (HCRAG_FAIL_MULTI_ADD)");
     if (rc != HCR_OK) {
-      // shards 0..j-1 already hold their blocks under ids m->n + r: the call's ids are
-      // consumed (never handed out again), the failed blocks are simply absent
-      s.gids.resize(old);
-      m->n += n;
-      return rc;
+      const std::string msg = hcr_last_error();
+      for (int i = 0; i <= j; ++i) {
+        hcr_multi_shard& t = m->sh[i];
+        if (hcr_index_size(t.ix) > old_rows[i]) (void)hcr_index_truncate_internal(t.ix, old_rows[i]);
+        t.gids.resize(old_gids[i]);
+      }
+      return hcr_set_errorf(rc, "%s (hcr_multi_add rolled back: no row of the call was added)", msg.c_str());
     }
   }
   m->n += n;

@@ -115,7 +115,13 @@ class VectorIndex:
         self.id_offset = int(offset)
 
     def get_rows(self, row0: int = 0, n: int | None = None) -> np.ndarray:
-        """Decoded stored rows as float32 (what the index actually ranks)."""
+        """Decoded stored rows as float32 (what the index actually ranks).  With
+        ``normalize=True`` 16-bit rows are the input direction scaled to unit norm and rounded
+        once -- the scale picked from 17 values within (1 +- 2^-9) of 1/||row|| so that the
+        ROUNDED row's norm is closest to 1 (topk_kernels.h ingest_kernel) -- so they differ from
+        a plain normalise-then-round of the input by a rounding step; cosine ranks are unchanged
+        beyond the storage precision (tests/test_exact_gpu.py::test_normalized_16bit_store_ranks_
+        like_the_inputs)."""
         if n is None:
             n = len(self) - row0
         out = np.empty((n, self.dim), dtype=np.float32)

@@ -165,28 +165,44 @@ def chunk_text(text: str, max_chunk_size: int = 1000, overlap: int = 100) -> Lis
 
 def extract_pdf_text(pdf_path) -> str:
     """embedding_generator.py:218-276 when pdfplumber / PyPDF2 are importable ("Page n: ..."
-    lines; pdfplumber first, whitespace-collapsed); "" when neither reads the file."""
-    pages: List[str] = []
-    try:
-        import pdfplumber
-        with pdfplumber.open(pdf_path) as pdf:
-            for i, page in enumerate(pdf.pages):
-                t = page.extract_text()
-                if t and t.strip():
-                    pages.append(f"Page {i + 1}: " + " ".join(t.split()))
-    except Exception:
-        pages = []
-    if not "\n".join(pages).strip():
-        pages = []
+    lines; pdfplumber first, whitespace-collapsed); "" when neither reads the file.  As there, a
+    page whose extraction raises is skipped (:229-231, :250-252) and the pages read so far are
+    kept; only a failure to open the file empties the method's result."""
+    def pdfplumber_pages():
+        out: List[str] = []
+        try:
+            import pdfplumber
+            with pdfplumber.open(pdf_path) as pdf:
+                for i, page in enumerate(pdf.pages):
+                    try:
+                        t = page.extract_text()
+                    except Exception:                   # noqa: BLE001 -- this page only
+                        continue
+                    if t and t.strip():
+                        out.append(f"Page {i + 1}: " + " ".join(t.split()))
+        except Exception:                               # noqa: BLE001 -- open / import failed
+            return []
+        return out
+
+    def pypdf2_pages():
+        out: List[str] = []
         try:
             import PyPDF2
             with open(pdf_path, "rb") as fh:
                 for i, page in enumerate(PyPDF2.PdfReader(fh).pages):
-                    t = page.extract_text()
+                    try:
+                        t = page.extract_text()
+                    except Exception:                   # noqa: BLE001 -- this page only
+                        continue
                     if t.strip():
-                        pages.append(f"Page {i + 1}: {t.strip()}")
-        except Exception:
-            pages = []
+                        out.append(f"Page {i + 1}: {t.strip()}")
+        except Exception:                               # noqa: BLE001
+            return []
+        return out
+
+    pages = pdfplumber_pages()
+    if not "\n".join(pages).strip():
+        pages = pypdf2_pages()
     return "\n".join(pages)
 
 

@@ -30,6 +30,7 @@ scanning in Python.
 from __future__ import annotations
 
 import json
+import logging
 import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
@@ -38,6 +39,8 @@ import numpy as np
 
 from ._lib import HCR_SCORE_COSINE
 from .index import VectorIndex
+
+_log = logging.getLogger(__name__)
 
 MAX_TOP_K = 2048          # hcr_search's limit (exact for every k up to it)
 
@@ -253,18 +256,30 @@ class _GpuRows:
         self._maybe_compact()
 
     def _maybe_compact(self) -> None:
+        """Compaction after an add / delete that already took effect: a failure to rebuild (the
+        fresh index needs HBM for the live rows while the old one is still held) leaves the
+        tombstoned index in place -- every search stays exact, the rows stay masked -- and is
+        logged, so the caller's add / delete still succeeds."""
         nd = int(self.deleted.sum())
         if nd >= self.COMPACT_MIN and nd >= self.COMPACT_FRAC * len(self.ids):
-            self.compact()
+            try:
+                self.compact()
+            except Exception as exc:                    # noqa: BLE001 -- kept tombstoned
+                _log.warning("vector store compaction failed (%s); rows stay tombstoned", exc)
 
     def compact(self) -> None:
         """Re-ingest the live rows (their nodes' embeddings, in insertion order, so ties still
-        break by insertion order) into a fresh index; the tombstoned rows' HBM is released."""
+        break by insertion order) into a fresh index; the tombstoned rows' HBM is released.  On
+        failure the half-built index is closed and this object is unchanged."""
         live = np.flatnonzero(~self.deleted)
         fresh = VectorIndex(self.dim, dtype=self.dtype, device=self.device)
-        if live.size:
-            E = np.asarray([_node_embedding(self.nodes[r]) for r in live], dtype=np.float32)
-            fresh.add(E, normalize=self.normalize)
+        try:
+            if live.size:
+                E = np.asarray([_node_embedding(self.nodes[r]) for r in live], dtype=np.float32)
+                fresh.add(E, normalize=self.normalize)
+        except BaseException:
+            fresh.close()
+            raise
         old, self.index = self.index, fresh
         old.close()
         self.ids = [self.ids[r] for r in live]

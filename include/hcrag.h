@@ -190,6 +190,7 @@ typedef struct hcr_multi_index hcr_multi_index;
 int hcr_multi_create(int n_dev, const int* dev_ids, int dim, int dtype, int64_t capacity_rows,
                      hcr_multi_index** out);
 int hcr_multi_destroy(hcr_multi_index* m);
+/* All or nothing: on failure no row of the call is added (shards that took their block drop it). */
 int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, int rows_dtype, int normalize);
 int hcr_multi_set_rowmask(hcr_multi_index* m, const uint8_t* mask, int64_t n);
 int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_t nq, int k, int score_mode,

@@ -319,3 +319,80 @@ def test_k200_aggressive_seed():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "k200 ok" in r.stdout
+
+
+_MULTI_ROLLBACK = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import hcrag_amd as hc
+from oracle import cosine_topk as O
+rng = np.random.default_rng(3)
+N, D = 9000, 128
+E = rng.standard_normal((N, D)).astype(np.float32)
+Q = rng.standard_normal((8, D)).astype(np.float32)
+with hc.MultiDeviceIndex(D, [0, 0, 0], dtype="f16") as mx:
+    mx.add(E[:6000])
+    sizes = mx.shard_sizes()
+    try:
+        mx.add(E[6000:])                   # shard 1 (HCRAG_FAIL_MULTI_ADD=1) fails
+        raise SystemExit("the injected failure did not surface")
+    except RuntimeError as exc:
+        assert "rolled back" in str(exc), exc
+    assert len(mx) == 6000 and mx.shard_sizes() == sizes, (len(mx), mx.shard_sizes(), sizes)
+    with hc.VectorIndex(D, "f16") as ref:
+        ref.add(E[:6000])
+        R = ref.get_rows()
+    s, i = mx.search(Q, 20)
+    es, ei = O.cosine_topk(Q, R, 20)
+    assert np.array_equal(i, ei) and np.max(np.abs(s - es)) < 1e-12
+print("rollback ok")
+"""
+
+
+def test_multi_add_failure_rolls_back():
+    """a hcr_multi_add that fails on shard j after shards 0..j-1 took their blocks
+    adds nothing (those blocks are dropped; the call's ids are not consumed), so the index
+    answers as before the call (HCRAG_FAIL_MULTI_ADD injects the failure, child process)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _MULTI_ROLLBACK, root, os.path.join(root, "hc-rag_amd")],
+                       env=dict(os.environ, HCRAG_FAIL_MULTI_ADD="1"), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "rollback ok" in r.stdout
+
+
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_normalized_16bit_store_ranks_like_the_inputs(hc, dtype):
+    """the ingest's scale search (normalize=True, 16-bit rows: the scale within
+    (1 +- 2^-9) / ||row|| whose rounded row has the norm closest to 1) changes the stored values
+    against a plain normalise-then-round -- pinned here against the fp64 oracle over the INPUT
+    vectors (not get_rows()): near-ties at gaps of 2e-3 (f16) / 1e-2 (bf16), well above the
+    storage rounding, must come back in the inputs' order; and each stored row is the input
+    direction to within that rounding."""
+    rng = np.random.default_rng(17 if dtype == "f16" else 18)
+    D, B, k = 384, 16, 12
+    gap = 2e-3 if dtype == "f16" else 1e-2
+    Q = rng.standard_normal((B, D))
+    Q /= np.linalg.norm(Q, axis=1, keepdims=True)
+    rows = []
+    for b in range(B):                   # k rows per query at cosines 0.9 - j gap (near-ties)
+        for j in range(k):
+            z = rng.standard_normal(D)
+            z -= (z @ Q[b]) * Q[b]
+            z /= np.linalg.norm(z)
+            c = 0.9 - j * gap
+            rows.append((c * Q[b] + np.sqrt(1 - c * c) * z) * rng.uniform(0.5, 3.0))
+    E = np.concatenate([np.asarray(rows), rng.standard_normal((5000, D))]).astype(np.float32)
+    perm = rng.permutation(len(E))
+    E = E[perm]
+    with hc.VectorIndex(D, dtype) as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows().astype(np.float64)
+        s, i = ix.search(Q.astype(np.float32), k)
+    es, ei = O.cosine_topk(Q.astype(np.float32), E.astype(np.float64), k)
+    np.testing.assert_array_equal(i, ei)             # the inputs' ranking
+    np.testing.assert_allclose(s, es, rtol=0, atol=gap / 4)
+    En = E / np.linalg.norm(E, axis=1, keepdims=True)
+    cos = np.sum(R * En, axis=1) / np.linalg.norm(R, axis=1)
+    assert 1 - cos.min() < (2e-6 if dtype == "f16" else 5e-5)
+    assert np.abs(np.linalg.norm(R, axis=1) - 1).max() < (1e-3 if dtype == "f16" else 2e-3)

@@ -175,6 +175,43 @@ def test_pdf_without_extractor_embeds_the_failure_text(tmp_path):
     assert g.process_pdf_document(pdf, "M2", extract_text=lambda p: "Page 1: hello. " * 80) == 2
 
 
+def test_pdf_page_errors_skip_only_that_page(tmp_path, monkeypatch):
+    """embedding_generator.py:242-252: pdfplumber pages are read one by one and a page whose
+    extract_text raises is skipped, the others kept (ADVICE r3: one bad page emptied the PDF);
+    a PDF that cannot be opened falls through to PyPDF2, then to ""."""
+    import sys
+    import types
+    from hcrag_amd.ingest import extract_pdf_text
+
+    class Page:
+        def __init__(self, t):
+            self.t = t
+
+        def extract_text(self):
+            if self.t is None:
+                raise ValueError("bad page")
+            return self.t
+
+    class Doc:
+        pages = [Page("first  page\ntext"), Page(None), Page("third"), Page("   ")]
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+    fake = types.ModuleType("pdfplumber")
+    fake.open = lambda path: Doc()
+    monkeypatch.setitem(sys.modules, "pdfplumber", fake)
+    assert extract_pdf_text(tmp_path / "x.pdf") == "Page 1: first page text\nPage 3: third"
+
+    def boom(path):
+        raise OSError("cannot open")
+    fake.open = boom
+    monkeypatch.setitem(sys.modules, "PyPDF2", None)   # (import fails: neither reads it)
+    assert extract_pdf_text(tmp_path / "x.pdf") == ""
+
+
 def test_store_rejects_mismatched_lengths(tmp_path):
     with pytest.raises(ValueError):
         EmbeddingStore.save(str(tmp_path / "s"), np.zeros((2, 4)), ["a"], [{}, {}])

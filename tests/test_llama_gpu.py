@@ -118,3 +118,37 @@ def test_vector_store_deletes_compact_hbm():
     assert res.ids == [f"n{live[j]}" for j in ei[0]]
     np.testing.assert_allclose(res.similarities, es[0], rtol=0, atol=1e-12)
     assert res.ids[:2] == ["n17", "n2001"]
+
+
+def test_vector_store_compaction_failure_keeps_tombstones(monkeypatch):
+    """a compaction that fails (the fresh index's add raising, as an HBM allocation
+    would) must not fail the delete that triggered it: the half-built index is closed, the rows
+    stay tombstoned in the old index and the answers are still the oracle's over the live rows."""
+    import hcrag_amd.llama_compat as lc
+    from hcrag_amd.llama_compat import MI355XVectorStore, TextNodeLite, VectorStoreQuery
+    rng = np.random.default_rng(8)
+    n, D = 2500, 64
+    E = rng.standard_normal((n, D))
+    vs = MI355XVectorStore(D, dtype="f32")
+    vs.add([TextNodeLite(id_=f"n{i}", embedding=E[i].tolist(), metadata={"ref_doc_id": f"d{i // 2}"})
+            for i in range(n)])
+    closed = []
+
+    class FailingIndex(lc.VectorIndex):
+        def add(self, *a, **k):
+            raise MemoryError("simulated out of HBM")
+
+        def close(self):
+            closed.append(self)
+            super().close()
+    monkeypatch.setattr(lc, "VectorIndex", FailingIndex)
+    for d in range(10, 700):                              # 1380 tombstones: compaction attempts
+        vs.delete(f"d{d}")
+    assert closed                                         # the fresh index was closed
+    assert len(vs.client) == n                            # nothing re-ingested: tombstones kept
+    live = np.array([i for i in range(n) if not (20 <= i < 1400)])
+    q = E[1500] + 0.01 * rng.standard_normal(D)
+    res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=20))
+    es, ei = O.cosine_topk(q[None].astype(np.float32), E[live].astype(np.float32), 20)
+    assert res.ids == [f"n{live[j]}" for j in ei[0]]
+    np.testing.assert_allclose(res.similarities, es[0], rtol=0, atol=1e-12)
