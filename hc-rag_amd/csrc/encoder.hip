@@ -59,7 +59,9 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
 // HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
-struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false; };
+// HCRAG_SPLIT_EARLY: the split GEMM's stage pieces issued at the stage barrier (A/B).
+struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
+                  split_early = false; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -69,6 +71,7 @@ static const EncHooks& enc_hooks() {
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
+    t.split_early = getenv("HCRAG_SPLIT_EARLY") != nullptr;
     return t;
   }();
   return h;
@@ -345,7 +348,17 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
   const bool ft192 = can192 && (force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256));
   const int nft = (int)(rup(N, ft192 ? 192 : G4_T) / (ft192 ? 192 : G4_T));
   const dim3 grid((unsigned)(nft * ntt));
-  if constexpr (!can192) {
+  if (enc_hooks().split_early) {
+    if constexpr (!can192)
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
+                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
+    else if (ft192)
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, 192, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
+                         nft, bias, resid, out_h, out_f, ldo, oscale);
+    else
+      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
+                         nft, bias, resid, out_h, out_f, ldo, oscale);
+  } else if constexpr (!can192) {
     if (enc_hooks().gelu_liberf)
       hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
                          T, nft, bias, resid, out_h, out_f, ldo, oscale);

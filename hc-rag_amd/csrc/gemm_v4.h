@@ -341,7 +341,10 @@ __device__ __forceinline__ void g5_read6(uint32_t a, half8 (&av)[6]) {
 
 // LIBERF: the FFN1 epilogue's GELU with the library erff (~50 instructions) instead of erf_as
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
-template <int EPI, int FT = G4_T, bool LIBERF = false>
+// EARLY: the next stage's pieces all issued right after the stage barrier (under the whole
+// stage's MFMAs) instead of spread over the three products -- the last of those landed just
+// before the next stage's vmcnt(0) wait (HCRAG_SPLIT_EARLY, A/B).
+template <int EPI, int FT = G4_T, bool LIBERF = false, bool EARLY = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
@@ -422,6 +425,10 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
     const char* st = ring + (s & 1) * STAGE;
+    if constexpr (EARLY) {
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) issue_piece(s + 1, i);
+    }
     V av[MT], bq[NQ], bl[NQ];
     if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
     else g5_read6(lds_addr(st + WH + offA), av);
@@ -432,9 +439,11 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-    issue_piece(s + 1, 0);
-    issue_piece(s + 1, 1);
-    issue_piece(s + 1, 2);
+    if constexpr (!EARLY) {
+      issue_piece(s + 1, 0);
+      issue_piece(s + 1, 1);
+      issue_piece(s + 1, 2);
+    }
     // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
 #pragma unroll
     for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
@@ -442,9 +451,11 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    issue_piece(s + 1, 3);
-    issue_piece(s + 1, 4);
-    issue_piece(s + 1, 5);
+    if constexpr (!EARLY) {
+      issue_piece(s + 1, 3);
+      issue_piece(s + 1, 4);
+      issue_piece(s + 1, 5);
+    }
     // Xh . Wl'
     if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
     else g5_read6(lds_addr(st + WL + offA), av);
@@ -452,8 +463,10 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    issue_piece(s + 1, 6);
-    if constexpr (PPW == 8) issue_piece(s + 1, 7);
+    if constexpr (!EARLY) {
+      issue_piece(s + 1, 6);
+      if constexpr (PPW == 8) issue_piece(s + 1, 7);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
