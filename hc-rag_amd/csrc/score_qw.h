@@ -98,7 +98,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp,
-                     int tstride = 1, float* __restrict__ umax = nullptr) {
+                     int tstride = 1, float* __restrict__ umax = nullptr, int old_test = 0) {
   using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
@@ -310,19 +310,33 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       }
       continue;
     }
-    float thr[2];
-    thr[0] = fmaxf(tkr[0] ? key_score(tkr[0]) : -INFINITY, unord32(tg2[0]));
-    thr[1] = fmaxf(tkr[1] ? key_score(tkr[1]) : -INFINITY, unord32(tg2[1]));
+    // the stage test as QW1's (r04): v_max3 over the raw accumulators and the threshold as an
+    // ordered key, max(high word of the local k'-th key, global bound) -- no fmaxf sNaN
+    // canonicalisation, no key -> float round trips (a NaN maximum passes; its scores fail below)
     bool hit[2];
+    if (old_test) {                // (the r03 test, A/B hook HCRAG_QW_OLDTEST)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      float mx = -INFINITY;
+      for (int n = 0; n < 2; ++n) {
+        const float th = fmaxf(tkr[n] ? key_score(tkr[n]) : -INFINITY, unord32(tg2[n]));
+        float mx = -INFINITY;
 #pragma unroll
-      for (int m = 0; m < RB; ++m)
-        mx = fmaxf(mx, fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])));
-      hit[n] = mx >= thr[n];
+        for (int m = 0; m < RB; ++m)
+          mx = fmaxf(mx, fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])));
+        hit[n] = mx >= th;
+      }
+    } else {
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        float mx = qw_max4(acc[0][n]);
+#pragma unroll
+        for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
+        hit[n] = qw_ord32(mx) >= max((uint32_t)(tkr[n] >> 32), tg2[n]);
+      }
     }
     if (__any(hit[0] || hit[1])) {
+      float thr[2];
+      thr[0] = unord32(max((uint32_t)(tkr[0] >> 32), tg2[0]));
+      thr[1] = unord32(max((uint32_t)(tkr[1] >> 32), tg2[1]));
       const uint32_t row0u = (uint32_t)row0;
 #pragma unroll
       for (int n = 0; n < 2; ++n) {

@@ -14,12 +14,17 @@ using namespace hcr;
 
 namespace {
 
+int old_test() {              // HCRAG_QW_OLDTEST (A/B hook, read once): the r03 stage test
+  static const int v = getenv("HCRAG_QW_OLDTEST") ? 1 : 0;
+  return v;
+}
+
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
   if constexpr (256 % SR != 0) {   // (a dense-only stage shape: the pre-pass never asks for it)
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                        static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr, old_test());
   } else if (a.umax)       // the sampling pre-pass (MAXONLY)
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                        st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
@@ -27,7 +32,8 @@ void launch_t(const QsArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                        static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr,
+                       old_test());
 }
 
 // Dense-pass stage shape at D = 768 (HCRAG_QW_SR, read once; test / A-B hook): 32 rows (48 KiB)
