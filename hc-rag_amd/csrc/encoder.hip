@@ -38,6 +38,22 @@ struct EncLayer {
   float sqkv = 1.f, so = 1.f, si = 1.f, so2 = 1.f;
 };
 
+// One sub-batch's activations and the stream its layers run on (hcr_encode_device splits a
+// batch over kEncSplits streams: the GEMMs' partly filled last rounds of one sub-batch are then
+// filled by the other's workgroups).
+struct EncWork {
+  DevBuf x, xh, qkv, ctx, inter, y;
+  DevBuf pk_off, pk_map, pk_ok, pk_tot;   // token packing (pack_tokens_kernel)
+  hipStream_t st = nullptr;               // (split sub-batches only; the first runs unsplit
+  hipEvent_t done = nullptr;              //  batches on the caller's stream)
+  void release() {
+    DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot};
+    for (DevBuf* d : b) d->release();
+  }
+};
+static constexpr int kEncSplits = 2;
+static constexpr int64_t kEncSplitMinSeqs = 128;   // smaller batches run on one stream
+
 struct hcr_encoder {
   int device = 0;
   hcr_bert_config cfg{};
@@ -48,8 +64,9 @@ struct hcr_encoder {
   DevBuf wemb, pemb, temb, embg, embb;
   std::vector<EncLayer> layers;
   // workspace
-  DevBuf ids, mask, x, xh, qkv, ctx, inter, y, out;
-  DevBuf pk_off, pk_map, pk_ok, pk_tot;   // token packing (pack_tokens_kernel)
+  DevBuf ids, mask, out;
+  EncWork work[kEncSplits];
+  hipEvent_t ev_in = nullptr;             // the caller's stream reached the batch
   size_t att_lds_limit = 64 * 1024;
 };
 
@@ -60,8 +77,9 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
 // HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
 // HCRAG_SPLIT_EARLY: the split GEMM's stage pieces issued at the stage barrier (A/B).
+// HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  split_early = false; };
+                  split_early = false; int streams = 0; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -72,6 +90,7 @@ static const EncHooks& enc_hooks() {
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
     t.split_early = getenv("HCRAG_SPLIT_EARLY") != nullptr;
+    if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
     return t;
   }();
   return h;
@@ -113,9 +132,15 @@ extern "C" int hcr_encoder_destroy(hcr_encoder* e) {
   if (!e) return HCR_OK;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  DevBuf* bufs[] = {&e->wemb, &e->pemb, &e->temb, &e->embg, &e->embb, &e->ids, &e->mask, &e->x,
-                    &e->xh, &e->qkv, &e->ctx, &e->inter, &e->y, &e->out};
+  DevBuf* bufs[] = {&e->wemb, &e->pemb, &e->temb, &e->embg, &e->embb, &e->ids, &e->mask, &e->out};
   for (DevBuf* b : bufs) b->release();
+  for (EncWork& w : e->work) {
+    if (w.st) (void)hipStreamSynchronize(w.st);
+    w.release();
+    if (w.done) (void)hipEventDestroy(w.done);
+    if (w.st) (void)hipStreamDestroy(w.st);
+  }
+  if (e->ev_in) (void)hipEventDestroy(e->ev_in);
   for (auto& L : e->layers) {
     DevBuf* lb[] = {&L.wqkv, &L.bqkv, &L.wo, &L.bo, &L.ln1g, &L.ln1b, &L.wi, &L.bi, &L.wo2, &L.bo2, &L.ln2g, &L.ln2b};
     for (DevBuf* b : lb) b->release();
@@ -377,30 +402,30 @@ static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N,
 }
 
 template <typename TM, int DH, int KB>
-static int launch_attention_mfma(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
+static int launch_attention_mfma(hcr_encoder* e, EncWork& w, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                                  hipStream_t st) {
   const size_t lds = attention_mfma_lds<TM, DH>(S);
   if (lds > 64 * 1024)
     HIPC(hipFuncSetAttribute((const void*)attention_mfma_kernel<TM, DH, KB>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipLaunchKernelGGL((attention_mfma_kernel<TM, DH, KB>), dim3((unsigned)(n * e->cfg.heads)),
-                     dim3(256), lds, st, e->qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden,
-                     e->cfg.heads, e->ctx.as<TM>());
+                     dim3(256), lds, st, w.qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden,
+                     e->cfg.heads, w.ctx.as<TM>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
 // Fast modes: MFMA attention for head dims 32 / 64 up to 512 keys, the scalar kernel otherwise.
 template <typename TM>
-static int launch_attention(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
+static int launch_attention(hcr_encoder* e, EncWork& w, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                             hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
   const int Sp = (S + 31) & ~31;
   if ((dh == 32 || dh == 64) && Sp <= 512) {
-    if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, d_mask, seq_off, n, S, st)
-                                   : launch_attention_mfma<TM, 32, 32>(e, d_mask, seq_off, n, S, st);
-    return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, d_mask, seq_off, n, S, st)
-                     : launch_attention_mfma<TM, 64, 32>(e, d_mask, seq_off, n, S, st);
+    if (dh == 32) return Sp <= 128 ? launch_attention_mfma<TM, 32, 8>(e, w, d_mask, seq_off, n, S, st)
+                                   : launch_attention_mfma<TM, 32, 32>(e, w, d_mask, seq_off, n, S, st);
+    return Sp <= 128 ? launch_attention_mfma<TM, 64, 8>(e, w, d_mask, seq_off, n, S, st)
+                     : launch_attention_mfma<TM, 64, 32>(e, w, d_mask, seq_off, n, S, st);
   }
   const size_t lds = (size_t)(5 * S + 4 * dh) * 4 + (size_t)2 * S * dh * sizeof(TM);
   if (lds > 160 * 1024) return hcr_set_errorf(HCR_EINVAL, "sequence length %d too long for attention LDS", S);
@@ -408,13 +433,13 @@ static int launch_attention(hcr_encoder* e, const int32_t* d_mask, const int32_t
     HIPC(hipFuncSetAttribute((const void*)attention_kernel<TM>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   hipLaunchKernelGGL((attention_kernel<TM>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                     e->qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<TM>());
+                     w.qkv.as<const TM>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, w.ctx.as<TM>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
 // Reference-precision mode: fp32 attention, K/V in LDS when the sequence fits.
-static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
+static int launch_attention_f32(hcr_encoder* e, EncWork& w, const int32_t* d_mask, const int32_t* seq_off, int64_t n, int S,
                                 hipStream_t st) {
   const int dh = e->cfg.hidden / e->cfg.heads;
   if (S <= 64 && (dh == 32 || dh == 64)) {      // short sequences: f32 MFMA tiles
@@ -423,8 +448,8 @@ static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, const int
     const unsigned grid = (unsigned)(n * e->cfg.heads);
 #define HCR_ATT_MFMA(DH_, NT_)                                                                    \
   hipLaunchKernelGGL((attention_f32_mfma_kernel<DH_, NT_>), dim3(grid), dim3(64), lds, st,        \
-                     e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads,            \
-                     e->ctx.as<_Float16>())
+                     w.qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads,            \
+                     w.ctx.as<_Float16>())
     if (dh == 64) {
       switch (nt) { case 1: HCR_ATT_MFMA(64, 1); break; case 2: HCR_ATT_MFMA(64, 2); break;
                     case 3: HCR_ATT_MFMA(64, 3); break; default: HCR_ATT_MFMA(64, 4); break; }
@@ -443,20 +468,20 @@ static int launch_attention_f32(hcr_encoder* e, const int32_t* d_mask, const int
   if (lds > 64 * 1024) HIPC(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   if (kv_lds)
     hipLaunchKernelGGL((attention_f32_kernel<true>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                       e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+                       w.qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, w.ctx.as<_Float16>());
   else
     hipLaunchKernelGGL((attention_f32_kernel<false>), dim3((unsigned)(n * e->cfg.heads)), dim3(256), lds, st,
-                       e->qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, e->ctx.as<_Float16>());
+                       w.qkv.as<const float>(), d_mask, seq_off, S, e->cfg.hidden, e->cfg.heads, w.ctx.as<_Float16>());
   HIPC(hipGetLastError());
   return HCR_OK;
 }
 
 template <typename TM, bool SPLIT>
-static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask, int64_t n, int S,
+static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int32_t* d_mask, int64_t n, int S,
                     float* d_out, hipStream_t st) {
   const auto& c = e->cfg;
   const int H = c.hidden, F = c.intermediate;
-  const int w = SPLIT ? 3 : 1;                        // activation row width factor
+  const int aw = SPLIT ? 3 : 1;                       // activation row width factor
   int64_t T = n * (int64_t)S;
   if (T > (int64_t)1 << 30) return hcr_set_error(HCR_EINVAL, "batch too large");
   // Token packing (pack_tokens_kernel): only the tokens the result depends on run through the
@@ -466,103 +491,103 @@ static int encode_t(hcr_encoder* e, const int32_t* d_ids, const int32_t* d_mask,
   const int32_t* seq_off = nullptr;
   const int32_t* key_mask = d_mask;                   // per-row key bits: padded mask or packed
   if (!enc_hooks().padded) {
-    CHECK(e->pk_off.ensure((size_t)(n + 1) * 4));
-    CHECK(e->pk_map.ensure((size_t)T * 4));
-    CHECK(e->pk_ok.ensure((size_t)T * 4));
-    CHECK(e->pk_tot.ensure(4));
+    CHECK(w.pk_off.ensure((size_t)(n + 1) * 4));
+    CHECK(w.pk_map.ensure((size_t)T * 4));
+    CHECK(w.pk_ok.ensure((size_t)T * 4));
+    CHECK(w.pk_tot.ensure(4));
     hipLaunchKernelGGL(pack_tokens_kernel, dim3(1), dim3(1024), 0, st, d_mask, n, S, c.pooling == 1 ? 1 : 0,
-                       e->pk_off.as<int32_t>(), e->pk_map.as<int32_t>(), e->pk_ok.as<int32_t>(),
-                       e->pk_tot.as<int32_t>());
+                       w.pk_off.as<int32_t>(), w.pk_map.as<int32_t>(), w.pk_ok.as<int32_t>(),
+                       w.pk_tot.as<int32_t>());
     HIPC(hipGetLastError());
     int32_t tot = 0;
-    HIPC(hipMemcpyAsync(&tot, e->pk_tot.p, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&tot, w.pk_tot.p, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     T = tot;
-    tok_map = e->pk_map.as<const int32_t>();
-    seq_off = e->pk_off.as<const int32_t>();
-    key_mask = e->pk_ok.as<const int32_t>();
+    tok_map = w.pk_map.as<const int32_t>();
+    seq_off = w.pk_off.as<const int32_t>();
+    key_mask = w.pk_ok.as<const int32_t>();
   }
   if (T == 0) {                  // no token reaches the output (mean pooling, every mask 0)
-    hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st, e->x.as<const float>(),
+    hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st, w.x.as<const float>(),
                        key_mask, seq_off, S, H, c.pooling, c.normalize, d_out);
     HIPC(hipGetLastError());
     return HCR_OK;
   }
   const int64_t Tp = rup(T, 256);
-  CHECK(e->x.ensure((size_t)Tp * H * 4));
-  CHECK(e->y.ensure((size_t)Tp * H * 4));
-  CHECK(e->xh.ensure((size_t)Tp * H * w * sizeof(TM)));
-  CHECK(e->ctx.ensure((size_t)Tp * H * w * sizeof(TM)));
-  CHECK(e->qkv.ensure((size_t)Tp * 3 * H * (SPLIT ? 4 : sizeof(TM))));
-  CHECK(e->inter.ensure((size_t)Tp * F * w * sizeof(TM)));
+  CHECK(w.x.ensure((size_t)Tp * H * 4));
+  CHECK(w.y.ensure((size_t)Tp * H * 4));
+  CHECK(w.xh.ensure((size_t)Tp * H * aw * sizeof(TM)));
+  CHECK(w.ctx.ensure((size_t)Tp * H * aw * sizeof(TM)));
+  CHECK(w.qkv.ensure((size_t)Tp * 3 * H * (SPLIT ? 4 : sizeof(TM))));
+  CHECK(w.inter.ensure((size_t)Tp * F * aw * sizeof(TM)));
   const unsigned gT = (unsigned)((T + 3) / 4);
   // vectorised LayerNorm kernels when H % 4 == 0 and H <= 1024 (all BERT widths here)
   const bool ln4 = (H % 4 == 0) && H <= 1024 && !enc_hooks().ln_scalar;
   auto layer_norm = [&](const DevBuf& g, const DevBuf& bb) {
     if (ln4)
-      hipLaunchKernelGGL((layernorm4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+      hipLaunchKernelGGL((layernorm4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, w.y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
-                         e->x.as<float>(), e->xh.as<TM>());
+                         w.x.as<float>(), w.xh.as<TM>());
     else
-      hipLaunchKernelGGL((layernorm_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, e->y.as<const float>(),
+      hipLaunchKernelGGL((layernorm_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, w.y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
-                         e->x.as<float>(), e->xh.as<TM>());
+                         w.x.as<float>(), w.xh.as<TM>());
   };
   if (ln4)
     hipLaunchKernelGGL((embed_ln4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
-                       e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+                       e->embb.as<const float>(), c.layer_norm_eps, w.x.as<float>(), w.xh.as<TM>());
   else
     hipLaunchKernelGGL((embed_ln_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
-                       e->embb.as<const float>(), c.layer_norm_eps, e->x.as<float>(), e->xh.as<TM>());
+                       e->embb.as<const float>(), c.layer_norm_eps, w.x.as<float>(), w.xh.as<TM>());
   HIPC(hipGetLastError());
   for (int l = 0; l < c.layers; ++l) {
     const EncLayer& L = e->layers[l];
     if constexpr (SPLIT) {
-      CHECK((launch_gemm_split<EPI_BIAS_F32>(L.wqkv.as<const _Float16>(), e->xh.as<const _Float16>(), H,
+      CHECK((launch_gemm_split<EPI_BIAS_F32>(L.wqkv.as<const _Float16>(), w.xh.as<const _Float16>(), H,
                                              3 * H, (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
-                                             e->qkv.as<float>(), 3 * H, L.sqkv, st)));
-      CHECK(launch_attention_f32(e, key_mask, seq_off, n, S, st));
+                                             w.qkv.as<float>(), 3 * H, L.sqkv, st)));
+      CHECK(launch_attention_f32(e, w, key_mask, seq_off, n, S, st));
     } else {
-      CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), e->xh.as<const TM>(), H, 3 * H, (int)T,
-                                       L.bqkv.as<const float>(), nullptr, e->qkv.as<TM>(), nullptr,
+      CHECK((launch_gemm<TM, EPI_BIAS>(L.wqkv.as<const TM>(), w.xh.as<const TM>(), H, 3 * H, (int)T,
+                                       L.bqkv.as<const float>(), nullptr, w.qkv.as<TM>(), nullptr,
                                        3 * H, L.sqkv, st)));
-      CHECK(launch_attention<TM>(e, key_mask, seq_off, n, S, st));
+      CHECK(launch_attention<TM>(e, w, key_mask, seq_off, n, S, st));
     }
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo.as<const _Float16>(), e->ctx.as<const _Float16>(), H, H,
-                                               (int)T, L.bo.as<const float>(), e->x.as<const float>(),
-                                               nullptr, e->y.as<float>(), H, L.so, st)));
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H, H,
+                                               (int)T, L.bo.as<const float>(), w.x.as<const float>(),
+                                               nullptr, w.y.as<float>(), H, L.so, st)));
     else
-      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), e->ctx.as<const TM>(), H, H,
-                                             (int)T, L.bo.as<const float>(), e->x.as<const float>(),
-                                             nullptr, e->y.as<float>(), H, L.so, st)));
+      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), w.ctx.as<const TM>(), H, H,
+                                             (int)T, L.bo.as<const float>(), w.x.as<const float>(),
+                                             nullptr, w.y.as<float>(), H, L.so, st)));
     layer_norm(L.ln1g, L.ln1b);
     HIPC(hipGetLastError());
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(L.wi.as<const _Float16>(), e->xh.as<const _Float16>(),
+      CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(L.wi.as<const _Float16>(), w.xh.as<const _Float16>(),
                                                     H, F, (int)T, L.bi.as<const float>(), nullptr,
-                                                    (_Float16*)e->inter.as<TM>(), nullptr, F, L.si, st)));
+                                                    (_Float16*)w.inter.as<TM>(), nullptr, F, L.si, st)));
     else
-      CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), e->xh.as<const TM>(), H, F, (int)T,
-                                            L.bi.as<const float>(), nullptr, e->inter.as<TM>(),
+      CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), w.xh.as<const TM>(), H, F, (int)T,
+                                            L.bi.as<const float>(), nullptr, w.inter.as<TM>(),
                                             nullptr, F, L.si, st)));
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo2.as<const _Float16>(), e->inter.as<const _Float16>(), F,
-                                               H, (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
-                                               nullptr, e->y.as<float>(), H, L.so2, st)));
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(), F,
+                                               H, (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
+                                               nullptr, w.y.as<float>(), H, L.so2, st)));
     else
-      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), e->inter.as<const TM>(), F, H,
-                                             (int)T, L.bo2.as<const float>(), e->x.as<const float>(),
-                                             nullptr, e->y.as<float>(), H, L.so2, st)));
+      CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), w.inter.as<const TM>(), F, H,
+                                             (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
+                                             nullptr, w.y.as<float>(), H, L.so2, st)));
     layer_norm(L.ln2g, L.ln2b);
     HIPC(hipGetLastError());
   }
   hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st,
-                     e->x.as<const float>(), key_mask, seq_off, S, H, c.pooling, c.normalize, d_out);
+                     w.x.as<const float>(), key_mask, seq_off, S, H, c.pooling, c.normalize, d_out);
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -577,9 +602,34 @@ extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int
   if (!d_ids || !d_mask || !d_out) return hcr_set_error(HCR_EINVAL, "NULL buffer");
   HIPC(hipSetDevice(e->device));
   hipStream_t st = (hipStream_t)stream;   // the caller's stream (NULL = legacy default)
-  if (e->dtype == HCR_F16) return encode_t<_Float16, false>(e, d_ids, d_mask, n, S, d_out, st);
-  if (e->dtype == HCR_BF16) return encode_t<__bf16, false>(e, d_ids, d_mask, n, S, d_out, st);
-  return encode_t<_Float16, true>(e, d_ids, d_mask, n, S, d_out, st);
+  auto run = [&](EncWork& w, int64_t s0, int64_t ns, hipStream_t ws) -> int {
+    const int32_t* ids = d_ids + s0 * S;
+    const int32_t* mask = d_mask + s0 * S;
+    float* out = d_out + s0 * e->cfg.hidden;
+    if (e->dtype == HCR_F16) return encode_t<_Float16, false>(e, w, ids, mask, ns, S, out, ws);
+    if (e->dtype == HCR_BF16) return encode_t<__bf16, false>(e, w, ids, mask, ns, S, out, ws);
+    return encode_t<_Float16, true>(e, w, ids, mask, ns, S, out, ws);
+  };
+  const int splits = (enc_hooks().streams == 1 || n < kEncSplitMinSeqs) ? 1 : kEncSplits;
+  if (splits == 1) return run(e->work[0], 0, n, st);
+  // Sub-batches of n / splits sequences, each on a stream of its own (ordered after the caller's
+  // work through ev_in; the caller's stream waits for every sub-batch's `done` event): every
+  // kernel of a sub-batch is a small grid whose partly filled last round of workgroups the other
+  // sub-batch's kernels fill, instead of leaving CUs idle.  Row-wise work and attention within a
+  // sequence do not depend on the split, so the embeddings are the same bits.
+  if (!e->ev_in) HIPC(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+  HIPC(hipEventRecord(e->ev_in, st));
+  for (int i = 0; i < splits; ++i) {
+    EncWork& w = e->work[i];
+    if (!w.st) HIPC(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
+    if (!w.done) HIPC(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+    HIPC(hipStreamWaitEvent(w.st, e->ev_in, 0));
+    const int64_t s0 = n * i / splits, s1 = n * (i + 1) / splits;
+    CHECK(run(w, s0, s1 - s0, w.st));
+    HIPC(hipEventRecord(w.done, w.st));
+  }
+  for (int i = 0; i < splits; ++i) HIPC(hipStreamWaitEvent(st, e->work[i].done, 0));
+  return HCR_OK;
 }
 
 extern "C" int hcr_encode(hcr_encoder* e, const int32_t* ids, const int32_t* mask, int64_t n, int S,

@@ -109,8 +109,9 @@ class BertEncoder:
         return out
 
     def encode_device(self, ids, mask, out, stream: Optional[int] = None) -> None:
-        """Device tensors (torch, int32 [n, S] / fp32 [n, hidden]); async on ``stream``
-        (a raw hipStream_t handle, default: torch's current stream)."""
+        """Device tensors (torch, int32 [n, S] / fp32 [n, hidden]) on ``stream`` (a raw
+        hipStream_t handle, default: torch's current stream).  The call reads the packed token
+        count back once (hcr_encode_device), then enqueues the layers asynchronously."""
         n, S = ids.shape
         if tuple(mask.shape) != (n, S) or tuple(out.shape) != (n, self.hidden):
             raise ValueError("shape mismatch")

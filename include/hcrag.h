@@ -260,8 +260,12 @@ int hcr_encoder_finalize(hcr_encoder* enc);
  * out: n x hidden fp32.  Synchronous, host buffers. */
 int hcr_encode(hcr_encoder* enc, const int32_t* ids, const int32_t* mask, int64_t n, int S,
                float* out);
-/* Same on device buffers, asynchronous on `stream` (a hipStream_t; NULL = the legacy default
- * stream).  Ids must be in [0, vocab_size). */
+/* Same on device buffers, on `stream` (a hipStream_t; NULL = the legacy default stream).  Ids
+ * must be in [0, vocab_size).  Only the tokens with mask 1 (plus position 0 under CLS pooling)
+ * run through the layers: the packed token count is read back once per call, so the call waits
+ * for the caller's earlier work on `stream` and for the packing kernel; the layers are then
+ * enqueued asynchronously (batches of >= 128 sequences split over two internal streams that
+ * `stream` waits for). */
 int hcr_encode_device(hcr_encoder* enc, const int32_t* d_ids, const int32_t* d_mask, int64_t n,
                       int S, float* d_out, void* stream);
 

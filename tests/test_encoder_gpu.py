@@ -393,3 +393,38 @@ def test_packed_tokens_mask_holes_and_masked_cls(dtype):
     for pool in ("mean", "cls"):
         enc = _encoder(conf, m, dtype, pooling=pool)
         _check(enc.encode_ids(ids, mask), _ref_embed(m, ids, mask, pool), dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_two_stream_split_bit_identical(tmp_path, dtype):
+    """Batches of >= 128 sequences are split over two streams (hcr_encode_device: each half's
+    kernels fill the other's partly filled last rounds); every sequence's embedding must be the
+    same bits as the one-stream run (HCRAG_ENC_STREAMS=1, child process), through encode_ids and
+    encode_device."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from hcrag_amd import config_from_hf
+    cfg = dict(BGE_BASE_2L, num_hidden_layers=2)
+    conf, m = _hf_model(cfg, 21)
+    rng = np.random.default_rng(21)
+    ids, mask = _batch(rng, 301, 32, cfg["vocab_size"])
+    enc = _encoder(conf, m, dtype, pooling="cls")
+    got = enc.encode_ids(ids, mask)
+    dev = torch.device("cuda:0")
+    out = torch.empty((301, cfg["hidden_size"]), dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream(dev)
+    enc.encode_device(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev), out, stream=s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), got)
+    inp = str(tmp_path / "in.npz")
+    np.savez(inp, ids=ids, mask=mask, dtype=dtype, cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
+             **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    one = str(tmp_path / "one.npy")
+    subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, one],
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="1"), check=True, timeout=240)
+    np.testing.assert_array_equal(got, np.load(one))
+    _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
