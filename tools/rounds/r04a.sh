@@ -11,4 +11,5 @@ $T r04a_bench 400 python bench.py && \
 $T r04a_qwt 200 tools/ab_env.sh r04a_qwt 1 HCRAG_QW_OLDTEST=1 X=0 && \
 $T r04a_ab 200 tools/ab_env.sh r04a_ab 1 HCRAG_QW_SR=32 HCRAG_QW_SR=48 && \
 $T r04a_enc 200 tools/ab_enc.sh r04a_enc 1 X=0 HCRAG_SPLIT_EARLY=1 && \
+$T r04a_enc2 200 tools/ab_enc.sh r04a_enc2 1 "HCRAG_ENC_PADDED=1 HCRAG_ENC_STREAMS=1" HCRAG_ENC_STREAMS=1 && \
 echo ALLDONE
