@@ -174,14 +174,15 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
     s.gids.resize(old + (size_t)(r1 - r0));
     for (int64_t r = r0; r < r1; ++r) s.gids[old + (size_t)(r - r0)] = m->n + r;
     // (test hook HCRAG_FAIL_MULTI_ADD=j: shard j's add fails after its rows went in, as an
-    // allocation failure part-way through would -- tests/test_exact_gpu.py)
+    // allocation failure part-way through would, in every add after the index's first --
+    // tests/test_exact_gpu.py)
     static const int fail_shard = [] {
       const char* e = getenv("HCRAG_FAIL_MULTI_ADD");
       return e ? atoi(e) : -1;
     }();
     int rc = hcr_index_add_ids(s.ix, (const char*)rows + (size_t)r0 * rb, r1 - r0, rows_dtype,
                                normalize, s.gids.data() + old);
-    if (rc == HCR_OK && j == fail_shard) rc = hcr_set_error(HCR_EHIP, "injected failure (HCRAG_FAIL_MULTI_ADD)");
+    if (rc == HCR_OK && j == fail_shard && m->n > 0) rc = hcr_set_error(HCR_EHIP, "injected failure (HCRAG_FAIL_MULTI_ADD)");
     if (rc != HCR_OK) {
       const std::string msg = hcr_last_error();
       for (int i = 0; i <= j; ++i) {
