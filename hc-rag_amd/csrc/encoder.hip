@@ -610,7 +610,11 @@ extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int
     if (e->dtype == HCR_BF16) return encode_t<__bf16, false>(e, w, ids, mask, ns, S, out, ws);
     return encode_t<_Float16, true>(e, w, ids, mask, ns, S, out, ws);
   };
-  const int splits = (enc_hooks().streams == 1 || n < kEncSplitMinSeqs) ? 1 : kEncSplits;
+  // r04a A/B (bge-base, 1024 x S = 32 ragged, one box): f16 142.3k -> 149.7-152.0k embeddings/s
+  // with the split, the f32 mode 66.2k -> 63.9k (its split GEMMs hold 128 KiB of LDS per
+  // workgroup and thrash each other's weights): split by default in the fast modes only
+  const int want = enc_hooks().streams > 0 ? enc_hooks().streams : (e->dtype == HCR_F32 ? 1 : kEncSplits);
+  const int splits = (want <= 1 || n < kEncSplitMinSeqs) ? 1 : kEncSplits;
   if (splits == 1) return run(e->work[0], 0, n, st);
   // Sub-batches of n / splits sequences, each on a stream of its own (ordered after the caller's
   // work through ev_in; the caller's stream waits for every sub-batch's `done` event): every

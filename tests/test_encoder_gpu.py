@@ -397,11 +397,12 @@ def test_packed_tokens_mask_holes_and_masked_cls(dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
-def test_two_stream_split_bit_identical(tmp_path, dtype):
+def test_two_stream_split_bit_identical(tmp_path, dtype, monkeypatch):
     """Batches of >= 128 sequences are split over two streams (hcr_encode_device: each half's
-    kernels fill the other's partly filled last rounds); every sequence's embedding must be the
-    same bits as the one-stream run (HCRAG_ENC_STREAMS=1, child process), through encode_ids and
-    encode_device."""
+    kernels fill the other's partly filled last rounds; the default in the fast modes, forced
+    here with HCRAG_ENC_STREAMS=2 for the f32 mode too -- the hook is read once per process, so
+    the split run is a child as well); every sequence's embedding must be the same bits as the
+    one-stream run (HCRAG_ENC_STREAMS=1, child process), through encode_ids and encode_device."""
     import json
     import os
     import subprocess
@@ -427,4 +428,8 @@ def test_two_stream_split_bit_identical(tmp_path, dtype):
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, one],
                    env=dict(os.environ, HCRAG_ENC_STREAMS="1"), check=True, timeout=240)
     np.testing.assert_array_equal(got, np.load(one))
+    two = str(tmp_path / "two.npy")
+    subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, two],
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="2"), check=True, timeout=240)
+    np.testing.assert_array_equal(got, np.load(two))
     _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
