@@ -348,9 +348,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     const int is = vt % L::NIS;
     const char* invl = lds + L::INV + is * L::INV_SLOT + lq * 16;
     const char* mskl = lds + L::MSK + is * 64;
-    if (((vt - t0) & 3) == 0) {
+    if (((vt - t0) & 3) == 0) {   // (from the opaque lane copy: a qlane-based address was spilled)
 #pragma unroll
-      for (int n = 0; n < NQ; ++n) tgr[n] = v3_lds_u32(lds + L::TG + is * L::TG_SLOT + (qlane + 16 * n) * 4);
+      for (int n = 0; n < NQ; ++n) tgr[n] = v3_lds_u32(lds + L::TG + is * L::TG_SLOT + (wq0 + (le & 15) + 16 * n) * 4);
     }
     float thr[NQ];
 #pragma unroll
@@ -382,31 +382,12 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         }
       }
     };
-    float mx[NQ];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) mx[n] = -INFINITY;
-    if (live) {
-      if constexpr (UNIT) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NQ; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r]);
-      } else {
-#pragma unroll
-        for (int m4 = 0; m4 < MT; m4 += 4) {
-          float4 iv[4];
-          qs_read_inv4(lds_addr(invl + m4 * 64), iv);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int n = 0; n < NQ; ++n)
-              mx[n] = fmaxf(mx[n], fmaxf(fmaxf(acc[m4 + i][n][0] * iv[i].x, acc[m4 + i][n][1] * iv[i].y),
-                                         fmaxf(acc[m4 + i][n][2] * iv[i].z, acc[m4 + i][n][3] * iv[i].w)));
-        }
-      }
-    } else {
+    // The tile's scores in place (r04): a UNIT corpus's whole tile is its raw accumulators;
+    // otherwise they are scaled by the rows' inverse norms (1 for UNIT) and set to NaN for rows
+    // past the corpus end or masked out (NaN never passes a >= test).  One epilogue path
+    // follows for every tile (r03 kept a checked twin of the whole epilogue: twice the append
+    // code, see below).
+    if (!(UNIT && live)) {
 #pragma unroll
       for (int m4 = 0; m4 < MT; m4 += 4) {
         float iv[4][4];
@@ -416,9 +397,18 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
           for (int n = 0; n < NQ; ++n)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m4 + i][n][r] * iv[i][r]);
+            for (int r = 0; r < 4; ++r) acc[m4 + i][n][r] *= iv[i][r];
       }
     }
+    float mx[NQ];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) mx[n] = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r]);
     bool hit[NQ];
     bool anyhit = false;
 #pragma unroll
@@ -431,11 +421,12 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     if (__any(anyhit)) {
       // a row is appended when its key beats the query's local k'-th key (same scores as the
       // max above: x * 1 == x, and the checked path equals the plain one on live rows).
-      // Unrolled (a run-time index into acc would put the accumulators in scratch), with
-      // wave-uniform tests: a tile usually holds one or two rows above a wave's bounds, yet the
-      // path is entered on ~93 % of the tiles (16 queries per wave); per-lane branches over
-      // all 64 elements cost ~8k cycles per tile, one uniform test per element ~5.3k (r02
-      // stamps), one per 4-row block (UNIT, live tile) ~3k.
+      // Code size (r04): the slow path had a checked twin for tail / masked / non-UNIT tiles,
+      // each with NQ x MT x 4 copies of the append: 62 KB of kernel code at configs[1], 90-100
+      // KB at KS = 24, against a 64 KB instruction cache shared by two CUs (every entry into
+      // the slow path missed in it: ~2.3k cycles per entry whatever the append did -- r04
+      // stamps with the appends staged in LDS: no change).  The scores are now made in place
+      // above, and one unrolled path serves every tile.
       auto append = [&](float sc, int m, int n, int r) __attribute__((always_inline)) {
         const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
         const uint64_t key = make_key(sc, rowl);
@@ -450,36 +441,26 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
       for (int n = 0; n < NQ; ++n) {
         if (!__any(hit[n])) continue;
-        if (UNIT && live) {
-          // one wave-uniform test per row block (its 4 rows' max, recomputed here: kept from
-          // the max above it costs 16 VGPRs, which the KS = 24 kernel spills)
+        // the row blocks holding a score at or above the threshold (a wave-uniform test per
+        // block, unrolled: no append code here), then one rolled loop over those blocks, block
+        // m's accumulators picked by a wave-uniform select, with the append body in it once
+        uint32_t blocks = 0;
 #pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            const bool cg = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])) >= thr[n];
-            if (__builtin_amdgcn_ballot_w64(cg)) {
-              if (cg) {
+        for (int m = 0; m < MT; ++m) {
+          const bool cg = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])) >= thr[n];
+          if (__builtin_amdgcn_ballot_w64(cg)) blocks |= 1u << m;
+        }
+#pragma unroll 1
+        while (blocks) {
+          const int m = __builtin_ctz(blocks);
+          blocks &= blocks - 1;
+          floatx4 v = acc[0][n];
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  if (acc[m][n][r] >= thr[n]) append(acc[m][n][r], m, n, r);
-              }
-            }
-          }
-        } else {
+          for (int mm = 1; mm < MT; ++mm)
+            if (m == mm) v = acc[mm][n];
 #pragma unroll
-          for (int m4 = 0; m4 < MT; m4 += 4) {
-            float iv[4][4];
-            checked4(m4, iv);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float sc = acc[m4 + i][n][r] * iv[i][r];
-                const bool c = sc >= thr[n];
-                if (__builtin_amdgcn_ballot_w64(c)) {
-                  if (c) append(sc, m4 + i, n, r);
-                }
-              }
-          }
+          for (int r = 0; r < 4; ++r)
+            if (v[r] >= thr[n]) append(v[r], m, n, r);
         }
       }
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
