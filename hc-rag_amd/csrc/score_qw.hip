@@ -36,13 +36,15 @@ void launch_t(const QsArgs& a, hipStream_t st) {
                        old_test());
 }
 
-// Dense-pass stage shape at D = 768 (HCRAG_QW_SR, read once; test / A-B hook): 32 rows (48 KiB)
-// in a 3-deep ring, or 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows instead of
-// per 32.  The MAXONLY pre-pass keeps 32-row stages (its units are 128 rows).
+// Dense-pass stage shape at D = 768: 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows
+// instead of per 32 (r04b A/B, 10M x 768 B = 1024, three interleaved rounds on one box: 13.19 /
+// 13.26 / 13.20 ms vs 13.21 / 13.38 / 13.30 with 32-row stages in a 3-deep ring); HCRAG_QW_SR=32
+// (read once; test / A-B hook) restores the 32-row form.  The MAXONLY pre-pass keeps 32-row
+// stages (its units are 128 rows).
 int dense_sr(int ks) {
   static const int sr = [] {
     const char* e = getenv("HCRAG_QW_SR");
-    return e ? atoi(e) : 32;
+    return e ? atoi(e) : 48;
   }();
   return ks == 24 && sr == 48 ? 48 : qw_sr(ks);
 }
