@@ -44,10 +44,12 @@ struct EncLayer {
 struct EncWork {
   DevBuf x, xh, qkv, ctx, inter, y;
   DevBuf pk_off, pk_map, pk_ok, pk_tot;   // token packing (pack_tokens_kernel)
+  DevBuf sk_ws, sk_sync;                  // split GEMM stream-K: a slab and a ticket + flag per
+                                          // workgroup-range boundary (zeroed once, never reset)
   hipStream_t st = nullptr;               // (split sub-batches only; the first runs unsplit
   hipEvent_t done = nullptr;              //  batches on the caller's stream)
   void release() {
-    DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot};
+    DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot, &sk_ws, &sk_sync};
     for (DevBuf* d : b) d->release();
   }
 };
@@ -68,6 +70,7 @@ struct hcr_encoder {
   EncWork work[kEncSplits];
   hipEvent_t ev_in = nullptr;             // the caller's stream reached the batch
   size_t att_lds_limit = 64 * 1024;
+  int ncu = 256;                          // compute units (stream-K grid of the split GEMM)
 };
 
 static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -76,10 +79,11 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
 // HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
-// HCRAG_SPLIT_EARLY: the split GEMM's stage pieces issued at the stage barrier (A/B).
+// HCRAG_SPLIT_NOSK: the split GEMM without its stream-K completion (whole tiles in rounds; A/B
+// and parity of the stream-K path).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  split_early = false; int streams = 0; };
+                  split_nosk = false, sk_diag = false; int streams = 0; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -89,7 +93,8 @@ static const EncHooks& enc_hooks() {
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
-    t.split_early = getenv("HCRAG_SPLIT_EARLY") != nullptr;
+    t.split_nosk = getenv("HCRAG_SPLIT_NOSK") != nullptr;
+    t.sk_diag = getenv("HCRAG_SK_DIAG") != nullptr;   // timing only: cut tiles' halves never meet
     if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
     return t;
   }();
@@ -119,6 +124,8 @@ extern "C" int hcr_encoder_create(int device, const hcr_bert_config* cfg, int co
   e->device = device;
   e->cfg = c;
   e->dtype = compute_dtype;
+  if (hipDeviceGetAttribute(&e->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || e->ncu <= 0)
+    e->ncu = 256;
   hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
   if (he != hipSuccess) {
     delete e;
@@ -355,48 +362,68 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 // epilogue) from the split operands (row length 3 K), on gemm_split_kernel (4 distinct tiles
 // per stage instead of the concatenated GEMM's 6).  Weights are padded to 768-row multiples (a
 // whole number of 256- or 192-feature tiles), T padded to 256.
+//
+// Decomposition: with more tiles than compute units and a partly filled last round, one
+// workgroup per CU runs all but the last two rounds' worth of tiles whole and splits the rest's
+// K steps evenly (stream-K, gemm_split_kernel).  bge-base at T ~ 24.6k: O / FFN2 291 tiles =
+// 1.14 tile-times per CU instead of 2 rounds, QKV 3.41 instead of 4, FFN1 4.55 instead of 5.
+struct SplitPlan { int ft, nft, grid, dp_tiles, sk_iters; };
+static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool sk) {
+  const int ntt = (int)(rup(T, G4_T) / G4_T);
+  // A round of 192-wide tiles costs ~0.86 of a 256 one (r02, bge-base T = 32768: QKV 6 rounds
+  // 354 us vs 5 rounds 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/): cost =
+  // tile-times per CU (fractional under stream-K) x that factor
+  auto tiles = [&](int ft) { return (int)(rup(N, ft) / ft) * ntt; };
+  auto cost = [&](int ft) {
+    const int t = tiles(ft);
+    const double r = (sk && t > ncu) ? (double)t / ncu : (double)((t + ncu - 1) / ncu);
+    return r * (ft == 192 ? 0.86 : 1.0);
+  };
+  SplitPlan p{};
+  p.ft = can192 && (force_ft ? force_ft == 192 : cost(192) < cost(256)) ? 192 : G4_T;
+  p.nft = (int)(rup(N, p.ft) / p.ft);
+  const int nt = p.nft * ntt;
+  if (!sk || nt <= ncu || nt % ncu == 0) {
+    p.grid = nt; p.dp_tiles = nt; p.sk_iters = 0;
+  } else {
+    // every stream-K range >= one tile's K steps: a tile is cut at most once
+    p.grid = ncu;
+    p.dp_tiles = (nt / ncu - 1) * ncu;
+    p.sk_iters = (nt - p.dp_tiles) * (K / V3_BK);
+  }
+  return p;
+}
+
 template <int EPI>
-static int launch_gemm_split(const _Float16* W, const _Float16* X, int K, int N, int T,
+static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Float16* X, int K, int N, int T,
                              const float* bias, const float* resid, _Float16* out_h, float* out_f,
                              int ldo, float oscale, hipStream_t st) {
   if (K % V3_BK) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM K=%d not a multiple of %d", K, V3_BK);
   if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
-  const int ntt = (int)(rup(T, G4_T) / G4_T);
-  // 192-feature tiles where they fill whole rounds of 256 resident workgroups and 256-wide
-  // ones do not (N = 768 at T = 32768: 512 tiles = 2 rounds vs 384 = 1.5).  A round of 192
-  // tiles costs ~0.86 of a 256 one (r02, bge-base T = 32768: QKV 6 rounds 354 us vs 5 rounds
-  // 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
-  auto rounds = [&](int ft) { return (double)((rup(N, ft) / ft * (int64_t)ntt + 255) / 256); };
-  const int force_ft = enc_hooks().gemm_ft;
   // (FFN1's epilogue stages 64-feature halves: 256-feature tiles only)
   constexpr bool can192 = EPI != EPI_BIAS_GELU_SPLIT;
-  const bool ft192 = can192 && (force_ft ? force_ft == 192 : rounds(192) * 0.86 < rounds(256));
-  const int nft = (int)(rup(N, ft192 ? 192 : G4_T) / (ft192 ? 192 : G4_T));
-  const dim3 grid((unsigned)(nft * ntt));
-  if (enc_hooks().split_early) {
-    if constexpr (!can192)
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
-                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
-    else if (ft192)
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, 192, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
-                         nft, bias, resid, out_h, out_f, ldo, oscale);
-    else
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, false, true>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
-                         nft, bias, resid, out_h, out_f, ldo, oscale);
-  } else if constexpr (!can192) {
-    if (enc_hooks().gelu_liberf)
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T, true>), grid, dim3(V3_NT), 0, st, W, X, K, N,
-                         T, nft, bias, resid, out_h, out_f, ldo, oscale);
-    else
-      hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), grid, dim3(V3_NT), 0, st, W, X, K, N, T,
-                         nft, bias, resid, out_h, out_f, ldo, oscale);
-  } else if (ft192) {
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, 192>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, nft,
-                       bias, resid, out_h, out_f, ldo, oscale);
-  } else {
-    hipLaunchKernelGGL((gemm_split_kernel<EPI, G4_T>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, nft,
-                       bias, resid, out_h, out_f, ldo, oscale);
+  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, !enc_hooks().split_nosk);
+  float* ws = nullptr;
+  uint32_t* sync = nullptr;
+  if (p.sk_iters) {
+    CHECK(w.sk_ws.ensure((size_t)ncu * G4_T * G4_T * 4));
+    CHECK(w.sk_sync.ensure((size_t)ncu * 2 * 4));
+    ws = w.sk_ws.as<float>();
+    sync = enc_hooks().sk_diag ? nullptr : w.sk_sync.as<uint32_t>();
   }
+  const dim3 grid((unsigned)p.grid);
+#define HCR_SPLIT(FT_, LIB_)                                                                        \
+  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, \
+                     p.nft, bias, resid, out_h, out_f, ldo, oscale, p.dp_tiles, p.sk_iters, ws, sync)
+  if constexpr (!can192) {
+    if (enc_hooks().gelu_liberf) HCR_SPLIT(G4_T, true);
+    else HCR_SPLIT(G4_T, false);
+  } else if (p.ft == 192) {
+    HCR_SPLIT(192, false);
+  } else {
+    HCR_SPLIT(G4_T, false);
+  }
+#undef HCR_SPLIT
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -547,7 +574,7 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
   for (int l = 0; l < c.layers; ++l) {
     const EncLayer& L = e->layers[l];
     if constexpr (SPLIT) {
-      CHECK((launch_gemm_split<EPI_BIAS_F32>(L.wqkv.as<const _Float16>(), w.xh.as<const _Float16>(), H,
+      CHECK((launch_gemm_split<EPI_BIAS_F32>(w, e->ncu, L.wqkv.as<const _Float16>(), w.xh.as<const _Float16>(), H,
                                              3 * H, (int)T, L.bqkv.as<const float>(), nullptr, nullptr,
                                              w.qkv.as<float>(), 3 * H, L.sqkv, st)));
       CHECK(launch_attention_f32(e, w, key_mask, seq_off, n, S, st));
@@ -558,7 +585,7 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
       CHECK(launch_attention<TM>(e, w, key_mask, seq_off, n, S, st));
     }
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H, H,
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H, H,
                                                (int)T, L.bo.as<const float>(), w.x.as<const float>(),
                                                nullptr, w.y.as<float>(), H, L.so, st)));
     else
@@ -568,7 +595,7 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
     layer_norm(L.ln1g, L.ln1b);
     HIPC(hipGetLastError());
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(L.wi.as<const _Float16>(), w.xh.as<const _Float16>(),
+      CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(w, e->ncu, L.wi.as<const _Float16>(), w.xh.as<const _Float16>(),
                                                     H, F, (int)T, L.bi.as<const float>(), nullptr,
                                                     (_Float16*)w.inter.as<TM>(), nullptr, F, L.si, st)));
     else
@@ -576,7 +603,7 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
                                             L.bi.as<const float>(), nullptr, w.inter.as<TM>(),
                                             nullptr, F, L.si, st)));
     if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(), F,
+      CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(), F,
                                                H, (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
                                                nullptr, w.y.as<float>(), H, L.so2, st)));
     else

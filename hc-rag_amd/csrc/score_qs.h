@@ -263,8 +263,12 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   // stale bound is a lower one (more appends, same lists)
   uint64_t tkr[NQ];
   uint32_t tgr[NQ];
+  // the lane's query's append count (r04: in registers -- the same in the query's 4 lanes --
+  // instead of an LDS atomic with return per append; cnt[] in LDS is written back before a
+  // compaction and at the end)
+  int cntr[NQ];
 #pragma unroll
-  for (int n = 0; n < NQ; ++n) { tkr[n] = 0; tgr[n] = 0; }
+  for (int n = 0; n < NQ; ++n) { tkr[n] = 0; tgr[n] = 0; cntr[n] = 0; }
   int s = 0;                                   // global stage index
   for (int vt = t0; vt < t1; ++vt) {
 #pragma unroll
@@ -427,17 +431,11 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       // the slow path missed in it: ~2.3k cycles per entry whatever the append did -- r04
       // stamps with the appends staged in LDS: no change).  The scores are now made in place
       // above, and one unrolled path serves every tile.
-      auto append = [&](float sc, int m, int n, int r) __attribute__((always_inline)) {
-        const uint32_t rowl = row0u + (uint32_t)(m * 16 + lq * 4 + r);
-        const uint64_t key = make_key(sc, rowl);
-        if (key > tkr[n]) {
-          const int ql = qlane + 16 * n;
-          const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-          if (pos < L::LS) v3_lds_store_u64(lds + L::SLOTS + (ql * L::LS + pos) * 8, key);
-          else wbuf[(size_t)ql * CAP + pos] = key;
-          need |= pos + 1 > CAP - RT;
-        }
-      };
+      // Appends without an LDS round trip (r04): the lanes of one query (lane & 15 equal: its 4
+      // row groups lq) take consecutive positions from the ballot of the hits -- a lane's
+      // position is the count so far plus the hits of the query's lanes below it (mbcnt) --
+      // and every lane adds the query's hit count to its copy of the counter.
+      const uint64_t qmask = 0x0001000100010001ull << (le & 15);
 #pragma unroll
       for (int n = 0; n < NQ; ++n) {
         if (!__any(hit[n])) continue;
@@ -450,6 +448,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
           const bool cg = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])) >= thr[n];
           if (__builtin_amdgcn_ballot_w64(cg)) blocks |= 1u << m;
         }
+        const int ql = qlane + 16 * n;
+        uint64_t* wq = wbuf + (size_t)ql * CAP;
+        char* sq = lds + L::SLOTS + ql * L::LS * 8;
 #pragma unroll 1
         while (blocks) {
           const int m = __builtin_ctz(blocks);
@@ -458,14 +459,31 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
           for (int mm = 1; mm < MT; ++mm)
             if (m == mm) v = acc[mm][n];
+          const uint32_t rowb = row0u + (uint32_t)(m * 16 + lq * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (v[r] >= thr[n]) append(v[r], m, n, r);
+          for (int r = 0; r < 4; ++r) {
+            // a row is appended when its key beats the query's local k'-th key (same scores as
+            // the max above: x * 1 == x, and the checked path equals the plain one on live rows)
+            const uint64_t key = make_key(v[r], rowb + (uint32_t)r);
+            const bool h = v[r] >= thr[n] && key > tkr[n];
+            const uint64_t bq = __builtin_amdgcn_ballot_w64(h) & qmask;
+            if (h) {
+              const int pos = cntr[n] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0u));
+              if (pos < L::LS) v3_lds_store_u64(sq + pos * 8, key);
+              else wq[pos] = key;
+            }
+            cntr[n] += __builtin_popcountll(bq);
+          }
         }
+        need |= cntr[n] > CAP - RT;
       }
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drain this wave's stores -- and, in order, its ring pieces -- only then)
       if (__any(need)) {
+#pragma unroll
+        for (int n = 0; n < NQ; ++n)
+          if (le < 16) v3_lds_store_u32(&cnt[qlane + 16 * n], (uint32_t)cntr[n]);
         flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -477,7 +495,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         }
         need = false;
 #pragma unroll
-        for (int n = 0; n < NQ; ++n) tkr[n] = v3_lds_u64(tau_key + qlane + 16 * n);
+        for (int n = 0; n < NQ; ++n) {
+          tkr[n] = v3_lds_u64(tau_key + qlane + 16 * n);
+          cntr[n] = (int)v3_lds_u32(cnt + qlane + 16 * n);
+        }
       }
     }
 #ifdef HCR_QS_STAMPS
@@ -496,6 +517,9 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
 
   // final: every query's surviving keys (at most k') appended to its region of the partials
+#pragma unroll
+  for (int n = 0; n < NQ; ++n)
+    if (lane < 16) v3_lds_store_u32(&cnt[qlane + 16 * n], (uint32_t)cntr[n]);
   flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");

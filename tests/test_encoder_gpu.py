@@ -424,12 +424,60 @@ def test_two_stream_split_bit_identical(tmp_path, dtype, monkeypatch):
     np.savez(inp, ids=ids, mask=mask, dtype=dtype, cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # the f32 mode's split GEMM cuts tiles' K ranges at points that depend on each stream's
+    # token count (stream-K, test_split_gemm_stream_k): the bit comparison runs on whole tiles
+    nosk = {"HCRAG_SPLIT_NOSK": "1"} if dtype == "f32" else {}
     one = str(tmp_path / "one.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, one],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="1"), check=True, timeout=240)
-    np.testing.assert_array_equal(got, np.load(one))
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="1", **nosk), check=True, timeout=240)
     two = str(tmp_path / "two.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, two],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="2"), check=True, timeout=240)
-    np.testing.assert_array_equal(got, np.load(two))
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="2", **nosk), check=True, timeout=240)
+    np.testing.assert_array_equal(np.load(one), np.load(two))
+    if dtype == "f32":
+        assert np.abs(got - np.load(one)).max() <= 1e-5
+    else:
+        np.testing.assert_array_equal(got, np.load(one))
     _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
+
+
+_NOSK_CHILD = _PADDED_CHILD
+
+
+@pytest.mark.gpu
+def test_split_gemm_stream_k(tmp_path):
+    """The reference-precision GEMM's stream-K completion (encoder.hip split_plan,
+    gemm_v4.h gemm_split_kernel / sk_meet): at T ~ 26k packed tokens every bge-base projection
+    has more tiles than compute units and a partly filled last round -- QKV and FFN1 run whole
+    tiles in rounds and then K-split ranges, O / FFN2 K-split ranges only (K = 768: 24 steps,
+    K = 3072: 96).  A cut tile's halves meet through a slot whichever arrives first, so two runs
+    are the same bits; the K split moves the fp32 sums by rounding only, so the embeddings stay
+    within 1e-5 of the whole-tile rounds (HCRAG_SPLIT_NOSK=1, child process: the hook is read once
+    per process) and within the f32 bar of fp32 BertModel."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from hcrag_amd import config_from_hf
+    cfg = dict(BGE_BASE_2L, num_hidden_layers=3)
+    conf, m = _hf_model(cfg, 31)
+    rng = np.random.default_rng(31)
+    n, S = 1100, 32
+    ids, mask = _batch(rng, n, S, cfg["vocab_size"], lens=rng.integers(16, S + 1, size=n))
+    assert int(mask.sum()) > 256 * 86           # > 85 token tiles: O / FFN2 have > 256 tiles
+    enc = _encoder(conf, m, "f32", pooling="cls")
+    a = enc.encode_ids(ids, mask)
+    b = enc.encode_ids(ids, mask)
+    np.testing.assert_array_equal(a, b)
+    inp = str(tmp_path / "in.npz")
+    np.savez(inp, ids=ids, mask=mask, dtype="f32", cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
+             **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    nosk = str(tmp_path / "nosk.npy")
+    subprocess.run([sys.executable, "-c", _NOSK_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, nosk],
+                   env=dict(os.environ, HCRAG_SPLIT_NOSK="1"), check=True, timeout=240)
+    c = np.load(nosk)
+    d = np.abs(a - c).max()
+    print(f"stream-K vs whole tiles: max |diff| = {d:.3e}")
+    assert d <= 1e-5, d
+    _check(a, _ref_embed(m, ids, mask, "cls"), "f32")
