@@ -365,22 +365,33 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 //
 // Decomposition: with more tiles than compute units and a partly filled last round, one
 // workgroup per CU runs all but the last two rounds' worth of tiles whole and splits the rest's
-// K steps evenly (stream-K, gemm_split_kernel).  bge-base at T ~ 24.6k: O / FFN2 291 tiles =
-// 1.14 tile-times per CU instead of 2 rounds, QKV 3.41 instead of 4, FFN1 4.55 instead of 5.
+// K steps evenly (stream-K, gemm_split_kernel).  bge-base at T ~ 24.6k (96 token tiles): O /
+// FFN2 288 256-wide tiles = 1.125 tile-times per CU instead of 2 rounds of 192-wide ones, QKV
+// 1152 192-wide tiles = 4.5 instead of 5 rounds, FFN1 4.5 instead of 5.  r04f (one box, kernel
+// traces): f32 encoder 63.6k -> 66.7k embeddings/s; the cut tiles' meeting (slab write + read)
+// costs ~12 us per GEMM (HCRAG_SK_DIAG, no meeting: 69.5k).
 struct SplitPlan { int ft, nft, grid, dp_tiles, sk_iters; };
 static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool sk) {
   const int ntt = (int)(rup(T, G4_T) / G4_T);
-  // A round of 192-wide tiles costs ~0.86 of a 256 one (r02, bge-base T = 32768: QKV 6 rounds
-  // 354 us vs 5 rounds 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/): cost =
-  // tile-times per CU (fractional under stream-K) x that factor
   auto tiles = [&](int ft) { return (int)(rup(N, ft) / ft) * ntt; };
-  auto cost = [&](int ft) {
-    const int t = tiles(ft);
-    const double r = (sk && t > ncu) ? (double)t / ncu : (double)((t + ncu - 1) / ncu);
-    return r * (ft == 192 ? 0.86 : 1.0);
-  };
+  bool use192;
+  if (force_ft) {
+    use192 = force_ft == 192;
+  } else if (sk && tiles(256) > ncu) {
+    // stream-K: tile-times per CU.  A 192-wide tile measured 0.75 of a 256 one (r04f, bge-base
+    // T = 24.6k, whole-tile rounds: 53 vs 71 us at K = 768), so the two tie at N = 768 / 2304;
+    // measured (same box): QKV (N = 2304) 256 us on 192-wide tiles vs 288 on 256, O / FFN2 (N =
+    // 768) 241 vs 235 -- ties go to 192 above N = 1024
+    const double c192 = tiles(192) * 0.75, c256 = tiles(256);
+    use192 = c192 < c256 || (c192 == c256 && N > 1024);
+  } else {
+    // whole-tile rounds: a round of 192-wide tiles cost ~0.86 of a 256 one (r02, T = 32768:
+    // QKV 6 rounds 354 us vs 5 rounds 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
+    auto rounds = [&](int ft) { return (double)((tiles(ft) + ncu - 1) / ncu); };
+    use192 = rounds(192) * 0.86 < rounds(256);
+  }
   SplitPlan p{};
-  p.ft = can192 && (force_ft ? force_ft == 192 : cost(192) < cost(256)) ? 192 : G4_T;
+  p.ft = can192 && use192 ? 192 : G4_T;
   p.nft = (int)(rup(N, p.ft) / p.ft);
   const int nt = p.nft * ntt;
   if (!sk || nt <= ncu || nt % ncu == 0) {

@@ -92,26 +92,6 @@ __device__ __forceinline__ void v3_lds_store_u64(void* p, uint64_t x) {
   asm volatile("ds_write_b64 %0, %1" : : "v"(a), "v"(x) : "memory");
 }
 
-// Candidate appends staged in LDS (score_qs.h): the first LS slots of a query's candidate
-// buffer live in LDS, so the common append is a ds_write (lgkmcnt) instead of a global store,
-// which would sit in the vmcnt stream of the LDS-DMA ring (counted in issue order with the
-// ring's pieces) and hold up a later stage's wait for its write acknowledgement (~2.8k cycles
-// with every CU storing).  A compaction leaves k' >= 64 > LS keys, so a compacted query never
-// stages again; its tau_key (the k'-th key, non-zero) marks it.  flush_staged copies the staged
-// slots [0, min(cnt, LS)) of the never-compacted queries q0 .. q0 + nq - 1 to their global
-// buffers -- before a compaction and before the final lists; copying a slot twice writes the
-// same key -- and the caller then waits vmcnt(0) and fences before anything reads them.
-template <int LS, int CAP>
-__device__ __attribute__((noinline)) void flush_staged(const char* slots, const int* cnt, const uint64_t* tau_key,
-                                             uint64_t* wbuf, int q0, int nq, int lane) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int e = lane; e < nq * LS; e += 64) {
-    const int ql = q0 + e / LS, j = e % LS;
-    if (j < (int)v3_lds_u32(cnt + ql) && v3_lds_u64(tau_key + ql) == 0ull)
-      wbuf[(size_t)ql * CAP + j] = v3_lds_u64(slots + ((size_t)ql * LS + j) * 8);
-  }
-}
-
 // the 12 MFMA fragments of a stage (8 row blocks at a, 4 query blocks at b, 1 KiB apart), one
 // wait.  Inline asm: a compiler-visible LDS read after the loop's LDS-DMA would get a
 // vmcnt(0) in front of it, draining the ring.

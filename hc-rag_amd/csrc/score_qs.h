@@ -117,7 +117,7 @@ struct QsLayout {
   static constexpr int TAU = MSK + NIS * 64;               // u64 tau_key[QT]
   static constexpr int CNT = TAU + QT * 8;                 // int cnt[QT]
   static constexpr int LS = 8;                             // staged append slots per query
-  static constexpr int SLOTS = CNT + QT * 4;               // u64 slots[QT][LS] (flush_staged)
+  static constexpr int SLOTS = CNT + QT * 4;               // u64 slots[QT][LS] (staged appends)
   static constexpr int TOTAL = SLOTS + QT * LS * 8;
   static_assert(KS % HS == 0, "whole stages per tile");
   static_assert(TOTAL <= 160 * 1024, "LDS budget");
@@ -265,10 +265,31 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   uint32_t tgr[NQ];
   // the lane's query's append count (r04: in registers -- the same in the query's 4 lanes --
   // instead of an LDS atomic with return per append; cnt[] in LDS is written back before a
-  // compaction and at the end)
-  int cntr[NQ];
+  // compaction and at the end) and the count at its last flush: candidates at positions
+  // [flushed, flushed + LS) wait in the query's LDS slots (see flush_slots)
+  int cntr[NQ], flushed[NQ];
 #pragma unroll
-  for (int n = 0; n < NQ; ++n) { tkr[n] = 0; tgr[n] = 0; cntr[n] = 0; }
+  for (int n = 0; n < NQ; ++n) { tkr[n] = 0; tgr[n] = 0; cntr[n] = 0; flushed[n] = 0; }
+  // Staged appends to their global positions, 64 per store instruction: lane l copies slots
+  // (l >> 4) + 4 i of its query.  Why staged (r04): the ring's waits count this wave's vector
+  // memory operations in issue order, so every store instruction an epilogue issues (one per
+  // append step with a hit) pushes the next D - 1 stage waits past pieces of later stages --
+  // per-append global stores cost ~1k cycles of stage wait per tile at configs[1] (r03 diag).
+  // A flush issues NQ x LS / 4 store instructions, when a query's slots are half full.
+  auto flush_slots = [&](int lane4) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+      const int ql = qlane + 16 * n;
+      const int staged = min(cntr[n] - flushed[n], L::LS);
+#pragma unroll
+      for (int i = 0; i < L::LS / 4; ++i) {
+        const int j = lane4 + 4 * i;
+        if (j < staged)
+          wbuf[(size_t)ql * CAP + flushed[n] + j] = v3_lds_u64(lds + L::SLOTS + (ql * L::LS + j) * 8);
+      }
+      flushed[n] = cntr[n];
+    }
+  };
   int s = 0;                                   // global stage index
   for (int vt = t0; vt < t1; ++vt) {
 #pragma unroll
@@ -470,21 +491,30 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
             if (h) {
               const int pos = cntr[n] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0u));
-              if (pos < L::LS) v3_lds_store_u64(sq + pos * 8, key);
-              else wq[pos] = key;
+              const int sp = pos - flushed[n];
+#if defined(HCR_QS_STAMPS) && defined(HCR_QS_DIAG_NOSTORE)
+              asm volatile("; diag: no store" :: "v"(sp), "v"(key));   // (stamps diag build only)
+#else
+              if (sp < L::LS) v3_lds_store_u64(sq + sp * 8, key);
+              else wq[pos] = key;            // (the slots are full: rare)
+#endif
             }
             cntr[n] += __builtin_popcountll(bq);
           }
         }
         need |= cntr[n] > CAP - RT;
       }
+      bool half = false;
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) half |= cntr[n] - flushed[n] >= L::LS / 2;
+      if (__any(half) && !__any(need)) flush_slots(lq);
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drain this wave's stores -- and, in order, its ring pieces -- only then)
       if (__any(need)) {
+        flush_slots(lq);
 #pragma unroll
         for (int n = 0; n < NQ; ++n)
           if (le < 16) v3_lds_store_u32(&cnt[qlane + 16 * n], (uint32_t)cntr[n]);
-        flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -497,7 +527,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
         for (int n = 0; n < NQ; ++n) {
           tkr[n] = v3_lds_u64(tau_key + qlane + 16 * n);
-          cntr[n] = (int)v3_lds_u32(cnt + qlane + 16 * n);
+          cntr[n] = flushed[n] = (int)v3_lds_u32(cnt + qlane + 16 * n);
         }
       }
     }
@@ -517,10 +547,10 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
 
   // final: every query's surviving keys (at most k') appended to its region of the partials
+  flush_slots(lane >> 4);
 #pragma unroll
   for (int n = 0; n < NQ; ++n)
     if (lane < 16) v3_lds_store_u32(&cnt[qlane + 16 * n], (uint32_t)cntr[n]);
-  flush_staged<L::LS, CAP>(lds + L::SLOTS, cnt, tau_key, wbuf, wq0, 16 * NQ, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 16 * NQ, kp, lane, partials, pcnt, P, p);
