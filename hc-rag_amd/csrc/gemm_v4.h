@@ -394,19 +394,26 @@ __device__ __forceinline__ bool sk_meet(floatx4 (&acc)[MT][4], char* ring, float
     for (uint32_t spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch &&
                              spins < (1u << 22); ++spins)
       __builtin_amdgcn_s_sleep(2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  // every slab byte was stored write-through (sc1) and drained before the flag, and every load
+  // of it below is an sc1 load (past this CU's L1): no agent-scope acquire needed, only the
+  // compiler kept from hoisting the loads above the poll
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const float* src = slab + lane * 4;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    float4 p[NQ];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) p[n] = *reinterpret_cast<const float4*>(slab + ((m * NQ + n) * 64 + lane) * 4);
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-      acc[m][n][0] += p[n].x; acc[m][n][1] += p[n].y; acc[m][n][2] += p[n].z; acc[m][n][3] += p[n].w;
-    }
+    floatx4 p0, p1, p2, p3;
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off sc1\n\t"
+        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3)
+        : "v"(src + m * NQ * 256)
+        : "memory");
+    acc[m][0] += p0; acc[m][1] += p1; acc[m][2] += p2; acc[m][3] += p3;
   }
   return true;
 }

@@ -425,15 +425,19 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
             for (int r = 0; r < 4; ++r) acc[m4 + i][n][r] *= iv[i][r];
       }
     }
-    float mx[NQ];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) mx[n] = -INFINITY;
+    // per row block maxima (kept for the slow path's block test), then per query block
+    float bmx[MT][NQ], mx[NQ];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n)
+        bmx[m][n] = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3]));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx[n] = fmaxf(mx[n], acc[m][n][r]);
+    for (int n = 0; n < NQ; ++n) {
+      mx[n] = bmx[0][n];
+#pragma unroll
+      for (int m = 1; m < MT; ++m) mx[n] = fmaxf(mx[n], bmx[m][n]);
+    }
     bool hit[NQ];
     bool anyhit = false;
 #pragma unroll
@@ -465,10 +469,8 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         // m's accumulators picked by a wave-uniform select, with the append body in it once
         uint32_t blocks = 0;
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          const bool cg = fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])) >= thr[n];
-          if (__builtin_amdgcn_ballot_w64(cg)) blocks |= 1u << m;
-        }
+        for (int m = 0; m < MT; ++m)
+          if (__builtin_amdgcn_ballot_w64(bmx[m][n] >= thr[n])) blocks |= 1u << m;
         const int ql = qlane + 16 * n;
         uint64_t* wq = wbuf + (size_t)ql * CAP;
         char* sq = lds + L::SLOTS + ql * L::LS * 8;
@@ -481,23 +483,29 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
           for (int mm = 1; mm < MT; ++mm)
             if (m == mm) v = acc[mm][n];
           const uint32_t rowb = row0u + (uint32_t)(m * 16 + lq * 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
+          // this lane's rows of the block at or above the threshold; one of them per lane per
+          // pass, lowest first (r04: the typical entry has one hit in the wave, and the body
+          // once per row r cost ~2.3k cycles per entry in VALU issue alone)
+          const float t = thr[n];
+          uint32_t hm = (v[0] >= t ? 1u : 0u) | (v[1] >= t ? 2u : 0u) | (v[2] >= t ? 4u : 0u) |
+                        (v[3] >= t ? 8u : 0u);
+#pragma unroll 1
+          while (__any(hm != 0u)) {
+            const bool live = hm != 0u;
+            const uint32_t r = (uint32_t)__builtin_ctz(hm | 16u);
+            const float sc = r == 0u ? v[0] : r == 1u ? v[1] : r == 2u ? v[2] : v[3];
+            hm &= hm - 1u;
             // a row is appended when its key beats the query's local k'-th key (same scores as
             // the max above: x * 1 == x, and the checked path equals the plain one on live rows)
-            const uint64_t key = make_key(v[r], rowb + (uint32_t)r);
-            const bool h = v[r] >= thr[n] && key > tkr[n];
+            const uint64_t key = make_key(sc, rowb + r);
+            const bool h = live && key > tkr[n];
             const uint64_t bq = __builtin_amdgcn_ballot_w64(h) & qmask;
             if (h) {
               const int pos = cntr[n] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0u));
               const int sp = pos - flushed[n];
-#if defined(HCR_QS_STAMPS) && defined(HCR_QS_DIAG_NOSTORE)
-              asm volatile("; diag: no store" :: "v"(sp), "v"(key));   // (stamps diag build only)
-#else
               if (sp < L::LS) v3_lds_store_u64(sq + sp * 8, key);
               else wq[pos] = key;            // (the slots are full: rare)
-#endif
             }
             cntr[n] += __builtin_popcountll(bq);
           }
