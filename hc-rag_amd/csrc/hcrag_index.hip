@@ -566,7 +566,7 @@ static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bo
   if (opt_qw1 != 0 && unit_ok && qw1_ok && qw1_supported(ld) && nq >= 257)
     return {qw1_rows(ld), qw1_queries(ld), 0, false, false, true};
   if (nq >= qw_from && unit_ok && qw_ok && qw_supported(ld))
-    return {qw_rows(ld), kQwQueries, kQwStages, false, true};
+    return {qw_rows(ld, (nq + kQwQueries - 1) / kQwQueries), kQwQueries, kQwStages, false, true};
   // 17-256 queries: the query-stationary kernel (queries in VGPRs, only rows streamed through
   // LDS; 129-256 as two 128-query blocks per row partition).  Score ms, QS vs v3/v4
   // (profiles/r02/qs_ab.txt): 10M x 768 B = 32 2.75 vs 3.67, B = 128 2.82 vs 4.32, B = 160 4.42
@@ -950,7 +950,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   CHECK(refresh_norm_stats(ix));
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
-                          qwable && qw_cap(kp, ix->ld) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
+                          qwable && qw_cap(kp, ix->ld, (nq + kQwQueries - 1) / kQwQueries) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
                           ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qs);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   if (hooks().debug_cfg)
@@ -966,7 +966,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int nqpad = (int)(qw1 ? round_up(round_up(nq, tq), 256) : round_up(nq, qs ? 256 : tq));
   const int nqb = (int)round_up(nq, tq) / tq;
   const int ntiles = (int)((ix->n + tr - 1) / tr);
-  const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld) : qw1 ? qw1_cap(kp, ix->ld) : next_pow2(kp + tr);
+  const int cap = qs ? qs_cap(kp) : qw ? qw_cap(kp, ix->ld, nqb) : qw1 ? qw1_cap(kp, ix->ld) : next_pow2(kp + tr);
   const int wg_target = ver == 1 ? 512 : 256;
   // (QW: one workgroup per CU -- its LDS -- so at most 256 workgroups: one round)
   int P = qw1 ? qw1_partitions(nqb, ntiles)

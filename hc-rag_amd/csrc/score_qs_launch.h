@@ -38,9 +38,9 @@ constexpr int kQsRowTile = 256;       // row tile of the 1-block kernel (128 for
 // Wide query-stationary kernel (score_qw.h): 256 queries per workgroup held in VGPRs, full-K
 // row stages; UNIT corpora without a row mask, ld = 384 or 768.
 bool qw_supported(int ld);
-int qw_rows(int ld);                  // rows per stage of the dense pass (the kernel's row tile)
+int qw_rows(int ld, int nqb);         // rows per stage of the dense pass (the kernel's row tile)
 int qw_sample_rows(int ld);           // ... of its MAXONLY pre-pass (256-row sampled tiles)
-int qw_cap(int kp, int ld);           // candidate buffer slots per query (0: k' too large)
+int qw_cap(int kp, int ld, int nqb);  // candidate buffer slots per query (0: k' too large)
 int launch_qw(int dtype, const QsArgs& a, hipStream_t st);
 constexpr int kQwQueries = 256;       // queries per QW workgroup (= QW_QT)
 constexpr int kQwStages = 3;          // QW ring stages (= QW_NST)

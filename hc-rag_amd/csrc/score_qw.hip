@@ -38,15 +38,18 @@ void launch_t(const QsArgs& a, hipStream_t st) {
 
 // Dense-pass stage shape at D = 768: 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows
 // instead of per 32 (r04b A/B, 10M x 768 B = 1024, three interleaved rounds on one box: 13.19 /
-// 13.26 / 13.20 ms vs 13.21 / 13.38 / 13.30 with 32-row stages in a 3-deep ring); HCRAG_QW_SR=32
-// (read once; test / A-B hook) restores the 32-row form.  The MAXONLY pre-pass keeps 32-row
-// stages (its units are 128 rows).
-int dense_sr(int ks) {
+// 13.26 / 13.20 ms vs 13.21 / 13.38 / 13.30 with 32-row stages in a 3-deep ring) -- for batches
+// of several query blocks.  With one query block (B <= 256) every row tile comes from HBM once
+// and the 3-deep ring of 32-row stages keeps more of it in flight: 10M x 768 B = 256, 3.855 /
+// 3.859 vs 3.880 / 3.879 ms (r04h, two interleaved rounds).  HCRAG_QW_SR=32 (read once; test / A-B
+// hook) takes the 32-row form everywhere.  The MAXONLY pre-pass keeps 32-row stages (its units
+// are 128 rows).
+int dense_sr(int ks, int nqb) {
   static const int sr = [] {
     const char* e = getenv("HCRAG_QW_SR");
     return e ? atoi(e) : 48;
   }();
-  return ks == 24 && sr == 48 ? 48 : qw_sr(ks);
+  return ks == 24 && sr == 48 && nqb > 1 ? 48 : qw_sr(ks);
 }
 
 template <typename TM, int CAP>
@@ -54,7 +57,7 @@ bool by_ks(int ks, const QsArgs& a, hipStream_t st) {
   switch (ks) {
     case 12: launch_t<TM, CAP, 12>(a, st); return true;
     case 24:
-      if (!a.umax && dense_sr(24) == 48) launch_t<TM, CAP, 24, 48, 2>(a, st);
+      if (!a.umax && dense_sr(24, a.nqb) == 48) launch_t<TM, CAP, 24, 48, 2>(a, st);
       else launch_t<TM, CAP, 24>(a, st);
       return true;
     default: return false;
@@ -71,9 +74,9 @@ bool by_cap(const QsArgs& a, hipStream_t st) {
 }  // namespace
 
 bool qw_supported(int ld) { return ld % V3_BK == 0 && qw_sr(ld / V3_BK) > 0; }
-int qw_rows(int ld) { return dense_sr(ld / V3_BK); }
+int qw_rows(int ld, int nqb) { return dense_sr(ld / V3_BK, nqb); }
 int qw_sample_rows(int ld) { return qw_sr(ld / V3_BK); }
-int qw_cap(int kp, int ld) { return kp + dense_sr(ld / V3_BK) <= 256 ? 256 : 0; }   // 0: not supported
+int qw_cap(int kp, int ld, int nqb) { return kp + dense_sr(ld / V3_BK, nqb) <= 256 ? 256 : 0; }   // 0: not supported
 
 int launch_qw(int dtype, const QsArgs& a, hipStream_t st) {
   const bool ok = dtype == HCR_F16 ? by_cap<_Float16>(a, st) : by_cap<__bf16>(a, st);
