@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--enc-modes", default="f32,f16",
                    help="encoder compute modes to time: f32 (reference precision) and/or f16/bf16")
     p.add_argument("--enc-seq", type=int, default=32)
+    p.add_argument("--enc-seed", type=int, default=77,
+                   help="seed of the encoder leg's synthetic token lengths (the packed token count)")
     p.add_argument("--enc-steps", type=int, default=10)
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_score.json"),
                    help="PMC HBM-traffic summary (tools/pmc_summary.py --traffic) of this config")
@@ -620,7 +622,7 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     cfg = ENC_SHAPES[a.encoder]
     enc = hc.BertEncoder(cfg, random_bert_state(cfg), dtype=mode, device=dev.index)
     S = a.enc_seq
-    g = torch.Generator(device="cpu").manual_seed(77 + rank)
+    g = torch.Generator(device="cpu").manual_seed(a.enc_seed + rank)
     ids = torch.randint(1000, cfg["vocab_size"], (B, S), generator=g, dtype=torch.int32)
     lens = torch.randint(S // 2, S + 1, (B,), generator=g)
     mask = (torch.arange(S)[None, :] < lens[:, None]).to(torch.int32)

@@ -79,11 +79,11 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
 // HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
-// HCRAG_SPLIT_NOSK: the split GEMM without its stream-K completion (whole tiles in rounds; A/B
-// and parity of the stream-K path).
+// HCRAG_SPLIT_SK=1: the split GEMM's stream-K completion (off by default: r04n/r04o measured it
+// slower than whole-tile rounds at bge-base's token counts -- see launch_gemm_split).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  split_nosk = false, sk_diag = false; int streams = 0; };
+                  split_sk = false, sk_diag = false; int streams = 0; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -93,7 +93,7 @@ static const EncHooks& enc_hooks() {
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
-    t.split_nosk = getenv("HCRAG_SPLIT_NOSK") != nullptr;
+    t.split_sk = getenv("HCRAG_SPLIT_SK") != nullptr;
     t.sk_diag = getenv("HCRAG_SK_DIAG") != nullptr;   // timing only: cut tiles' halves never meet
     if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
     return t;
@@ -363,13 +363,17 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 // per stage instead of the concatenated GEMM's 6).  Weights are padded to 768-row multiples (a
 // whole number of 256- or 192-feature tiles), T padded to 256.
 //
-// Decomposition: with more tiles than compute units and a partly filled last round, one
-// workgroup per CU runs all but the last two rounds' worth of tiles whole and splits the rest's
-// K steps evenly (stream-K, gemm_split_kernel).  bge-base at T ~ 24.6k (96 token tiles): O /
-// FFN2 288 256-wide tiles = 1.125 tile-times per CU instead of 2 rounds of 192-wide ones, QKV
-// 1152 192-wide tiles = 4.5 instead of 5 rounds, FFN1 4.5 instead of 5.  r04f (one box, kernel
-// traces): f32 encoder 63.6k -> 66.7k embeddings/s; the cut tiles' meeting (slab write + read)
-// costs ~12 us per GEMM (HCRAG_SK_DIAG, no meeting: 69.5k).
+// Decomposition: whole 256- or 192-feature x 256-token tiles in rounds of one workgroup per CU
+// (the LDS ring holds one per CU).  A stream-K completion is built (HCRAG_SPLIT_SK=1): all but
+// the last two rounds' worth of tiles whole, then the remaining tiles' K steps split evenly over
+// one workgroup per CU, cut tiles' halves meeting through a workspace slot (gemm_split_kernel).
+// It balances the rounds (bge-base O / FFN2 at 96 token tiles: 1.125 tile-times per CU instead
+// of 2 rounds) but measured slower overall (r04n kernel traces, one box, 96 / 97 token tiles):
+// O / FFN2 236 vs 259 us at 96 but 263 vs 258 at 97, FFN1 347-361 vs 332-335, QKV 250-263 vs
+// 240-244, and the attention after a stream-K QKV 86 vs 78 us.  Workgroups that share a token
+// tile's activations run at different K offsets in the split ranges, so the activations are
+// fetched once per workgroup instead of once per round from L2, and the cut tiles' slabs (256
+// KiB each, read back in a burst at the launch's end) cost ~12 us per GEMM.  Default off.
 struct SplitPlan { int ft, nft, grid, dp_tiles, sk_iters; };
 static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool sk) {
   const int ntt = (int)(rup(T, G4_T) / G4_T);
@@ -379,11 +383,10 @@ static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force
     use192 = force_ft == 192;
   } else if (sk && tiles(256) > ncu) {
     // stream-K: tile-times per CU.  A 192-wide tile measured 0.75 of a 256 one (r04f, bge-base
-    // T = 24.6k, whole-tile rounds: 53 vs 71 us at K = 768), so the two tie at N = 768 / 2304;
-    // measured (same box): QKV (N = 2304) 256 us on 192-wide tiles vs 288 on 256, O / FFN2 (N =
-    // 768) 241 vs 235 -- ties go to 192 above N = 1024
-    const double c192 = tiles(192) * 0.75, c256 = tiles(256);
-    use192 = c192 < c256 || (c192 == c256 && N > 1024);
+    // T = 24.6k, whole-tile rounds: 53 vs 71 us at K = 768), so the two widths balance alike;
+    // the stream-K kernel keeps its registers at 192 (252 VGPRs, no spills) and spills at 256
+    // (256 VGPRs, 70-95 scratch accesses around the epilogue in its segment loop)
+    use192 = true;
   } else {
     // whole-tile rounds: a round of 192-wide tiles cost ~0.86 of a 256 one (r02, T = 32768:
     // QKV 6 rounds 354 us vs 5 rounds 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
@@ -413,7 +416,7 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
   if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
   // (FFN1's epilogue stages 64-feature halves: 256-feature tiles only)
   constexpr bool can192 = EPI != EPI_BIAS_GELU_SPLIT;
-  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, !enc_hooks().split_nosk);
+  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, enc_hooks().split_sk);
   float* ws = nullptr;
   uint32_t* sync = nullptr;
   if (p.sk_iters) {
@@ -422,18 +425,24 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
     ws = w.sk_ws.as<float>();
     sync = enc_hooks().sk_diag ? nullptr : w.sk_sync.as<uint32_t>();
   }
-  const dim3 grid((unsigned)p.grid);
-#define HCR_SPLIT(FT_, LIB_)                                                                        \
-  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_>), grid, dim3(V3_NT), 0, st, W, X, K, N, T, \
-                     p.nft, bias, resid, out_h, out_f, ldo, oscale, p.dp_tiles, p.sk_iters, ws, sync)
+  // the data-parallel rounds (whole tiles), then the stream-K launch over the rest
+#define HCR_SPLIT(FT_, LIB_, SK_, GRID_, BASE_)                                                    \
+  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_, SK_>), dim3((unsigned)(GRID_)), dim3(V3_NT), 0, st, \
+                     W, X, K, N, T, p.nft, bias, resid, out_h, out_f, ldo, oscale, BASE_, p.sk_iters, ws, sync)
+#define HCR_SPLIT_FT(FT_, LIB_)                                                                     \
+  do {                                                                                              \
+    if (p.dp_tiles > 0) HCR_SPLIT(FT_, LIB_, false, p.dp_tiles, 0);                                 \
+    if (p.sk_iters > 0) HCR_SPLIT(FT_, LIB_, true, p.grid, p.dp_tiles);                             \
+  } while (0)
   if constexpr (!can192) {
-    if (enc_hooks().gelu_liberf) HCR_SPLIT(G4_T, true);
-    else HCR_SPLIT(G4_T, false);
+    if (enc_hooks().gelu_liberf) HCR_SPLIT_FT(G4_T, true);
+    else HCR_SPLIT_FT(G4_T, false);
   } else if (p.ft == 192) {
-    HCR_SPLIT(192, false);
+    HCR_SPLIT_FT(192, false);
   } else {
-    HCR_SPLIT(G4_T, false);
+    HCR_SPLIT_FT(G4_T, false);
   }
+#undef HCR_SPLIT_FT
 #undef HCR_SPLIT
   HIPC(hipGetLastError());
   return HCR_OK;

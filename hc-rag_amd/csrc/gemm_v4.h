@@ -420,12 +420,17 @@ __device__ __forceinline__ bool sk_meet(floatx4 (&acc)[MT][4], char* ring, float
 
 // LIBERF: the FFN1 epilogue's GELU with the library erff (~50 instructions) instead of erf_as
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
-template <int EPI, int FT = G4_T, bool LIBERF = false>
+// SK = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index), the
+// data-parallel rounds; SK = true: the stream-K launch over tiles tile_base.. (sk_iters K steps
+// split evenly over the grid).  Two instantiations rather than one loop over both: the loop
+// around the epilogue cost the data-parallel tiles 12-16 % (256 VGPRs and spills against 191 and
+// none: r04m/r04n traces).
+template <int EPI, int FT = G4_T, bool LIBERF = false, bool SK = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
                   const float* __restrict__ resid, _Float16* __restrict__ out_h,
-                  float* __restrict__ out_f, int ldo, float oscale, int dp_tiles, int sk_iters,
+                  float* __restrict__ out_f, int ldo, float oscale, int tile_base, int sk_iters,
                   float* __restrict__ sk_ws, uint32_t* __restrict__ sk_sync) {
   using Op = MfmaOp<_Float16>;
   using V = half8;
@@ -445,9 +450,8 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int nsteps = K / V3_BK;
-  const int ndp = g < dp_tiles ? (dp_tiles - 1 - g) / nwg + 1 : 0;
-  const int sk_hi = (int)((int64_t)(g + 1) * sk_iters / nwg);
-  int pos = (int)((int64_t)g * sk_iters / nwg);
+  const int sk_hi = SK ? (int)((int64_t)(g + 1) * sk_iters / nwg) : 0;
+  int pos = SK ? (int)((int64_t)g * sk_iters / nwg) : 0;
 
   const int ldb = 3 * K * 2;                   // bytes per split row
   const int drow = lane >> 2;
@@ -461,18 +465,18 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   const int offB = (wn * 64 + fr) * 64 + fslot * 16;
 
   for (int j = 0;; ++j) {
-    // this workgroup's next segment: a whole data-parallel tile, or a piece of its K range
+    // this workgroup's next segment: its whole tile, or the next piece of its K range
     int tile, ks0, ks1;
-    if (j < ndp) {
-      tile = g + j * nwg; ks0 = 0; ks1 = nsteps;
-    } else if (pos < sk_hi) {
+    if constexpr (!SK) {
+      if (j > 0) break;
+      tile = g; ks0 = 0; ks1 = nsteps;
+    } else {
+      if (pos >= sk_hi) break;
       const int u = pos / nsteps;
-      tile = dp_tiles + u;
+      tile = tile_base + u;
       ks0 = pos - u * nsteps;
       ks1 = min(nsteps, ks0 + (sk_hi - pos));
       pos += ks1 - ks0;
-    } else {
-      break;
     }
     tile = __builtin_amdgcn_readfirstlane(tile);
     ks0 = __builtin_amdgcn_readfirstlane(ks0);
@@ -559,13 +563,15 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    if (ks0 > 0 || ks1 < nsteps) {
-      // a cut tile: slot = the range boundary inside it (this range's start or end)
-      const int slot = ks0 > 0 ? g : g + 1;
-      if (!sk_sync) {                 // (timing diagnostic HCRAG_SK_DIAG=1: no meeting, wrong sums)
-        if (ks0 > 0) continue;
-      } else if (!sk_meet<MT>(acc, ring, sk_ws + (size_t)slot * (FT * G4_T), sk_sync, slot, nwg, tid)) {
-        continue;
+    if constexpr (SK) {
+      if (ks0 > 0 || ks1 < nsteps) {
+        // a cut tile: slot = the range boundary inside it (this range's start or end)
+        const int slot = ks0 > 0 ? g : g + 1;
+        if (!sk_sync) {                 // (timing diagnostic HCRAG_SK_DIAG=1: no meeting, wrong sums)
+          if (ks0 > 0) continue;
+        } else if (!sk_meet<MT>(acc, ring, sk_ws + (size_t)slot * (FT * G4_T), sk_sync, slot, nwg, tid)) {
+          continue;
+        }
       }
     }
 

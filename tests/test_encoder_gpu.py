@@ -424,36 +424,42 @@ def test_two_stream_split_bit_identical(tmp_path, dtype, monkeypatch):
     np.savez(inp, ids=ids, mask=mask, dtype=dtype, cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    # the f32 mode's split GEMM cuts tiles' K ranges at points that depend on each stream's
-    # token count (stream-K, test_split_gemm_stream_k): the bit comparison runs on whole tiles
-    nosk = {"HCRAG_SPLIT_NOSK": "1"} if dtype == "f32" else {}
     one = str(tmp_path / "one.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, one],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="1", **nosk), check=True, timeout=240)
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="1"), check=True, timeout=240)
+    np.testing.assert_array_equal(got, np.load(one))
     two = str(tmp_path / "two.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, two],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="2", **nosk), check=True, timeout=240)
-    np.testing.assert_array_equal(np.load(one), np.load(two))
-    if dtype == "f32":
-        assert np.abs(got - np.load(one)).max() <= 1e-5
-    else:
-        np.testing.assert_array_equal(got, np.load(one))
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="2"), check=True, timeout=240)
+    np.testing.assert_array_equal(got, np.load(two))
     _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
 
 
-_NOSK_CHILD = _PADDED_CHILD
+_SK_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+d = np.load(sys.argv[3])
+from hcrag_amd import BertEncoder
+import json
+cfg = json.loads(str(d["cfg"]))
+state = {k[3:]: d[k] for k in d.files if k.startswith("sd_")}
+enc = BertEncoder(cfg, state, dtype=str(d["dtype"]))
+a = enc.encode_ids(d["ids"], d["mask"])
+b = enc.encode_ids(d["ids"], d["mask"])
+np.save(sys.argv[4], np.stack([a, b]))
+"""
 
 
 @pytest.mark.gpu
 def test_split_gemm_stream_k(tmp_path):
-    """The reference-precision GEMM's stream-K completion (encoder.hip split_plan,
-    gemm_v4.h gemm_split_kernel / sk_meet): at T ~ 26k packed tokens every bge-base projection
-    has more tiles than compute units and a partly filled last round -- QKV and FFN1 run whole
-    tiles in rounds and then K-split ranges, O / FFN2 K-split ranges only (K = 768: 24 steps,
-    K = 3072: 96).  A cut tile's halves meet through a slot whichever arrives first, so two runs
-    are the same bits; the K split moves the fp32 sums by rounding only, so the embeddings stay
-    within 1e-5 of the whole-tile rounds (HCRAG_SPLIT_NOSK=1, child process: the hook is read once
-    per process) and within the f32 bar of fp32 BertModel."""
+    """The reference-precision GEMM's stream-K completion (HCRAG_SPLIT_SK=1, off by default:
+    encoder.hip split_plan / launch_gemm_split, gemm_v4.h gemm_split_kernel<SK> / sk_meet): at
+    T ~ 26k packed tokens every bge-base projection has more tiles than compute units and a
+    partly filled last round -- QKV and FFN1 run whole tiles in rounds and then K-split ranges,
+    O / FFN2 K-split ranges only (K = 768: 24 steps, K = 3072: 96).  A cut tile's halves meet
+    through a slot whichever arrives first, so two runs are the same bits; the K split moves the
+    fp32 sums by rounding only, so the embeddings stay within 1e-5 of the whole-tile rounds (the
+    default, in this process) and within the f32 bar of fp32 BertModel."""
     import json
     import os
     import subprocess
@@ -466,17 +472,16 @@ def test_split_gemm_stream_k(tmp_path):
     ids, mask = _batch(rng, n, S, cfg["vocab_size"], lens=rng.integers(16, S + 1, size=n))
     assert int(mask.sum()) > 256 * 86           # > 85 token tiles: O / FFN2 have > 256 tiles
     enc = _encoder(conf, m, "f32", pooling="cls")
-    a = enc.encode_ids(ids, mask)
-    b = enc.encode_ids(ids, mask)
-    np.testing.assert_array_equal(a, b)
+    c = enc.encode_ids(ids, mask)
     inp = str(tmp_path / "in.npz")
     np.savez(inp, ids=ids, mask=mask, dtype="f32", cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    nosk = str(tmp_path / "nosk.npy")
-    subprocess.run([sys.executable, "-c", _NOSK_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, nosk],
-                   env=dict(os.environ, HCRAG_SPLIT_NOSK="1"), check=True, timeout=240)
-    c = np.load(nosk)
+    sk = str(tmp_path / "sk.npy")
+    subprocess.run([sys.executable, "-c", _SK_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, sk],
+                   env=dict(os.environ, HCRAG_SPLIT_SK="1"), check=True, timeout=240)
+    a, b = np.load(sk)
+    np.testing.assert_array_equal(a, b)
     d = np.abs(a - c).max()
     print(f"stream-K vs whole tiles: max |diff| = {d:.3e}")
     assert d <= 1e-5, d
