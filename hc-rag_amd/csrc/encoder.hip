@@ -16,6 +16,7 @@
 //                       fp32 accumulation), fp32 attention, library erff / expf.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -44,12 +45,12 @@ struct EncLayer {
 struct EncWork {
   DevBuf x, xh, qkv, ctx, inter, y;
   DevBuf pk_off, pk_map, pk_ok, pk_tot;   // token packing (pack_tokens_kernel)
-  DevBuf sk_ws, sk_sync;                  // split GEMM stream-K: a slab and a ticket + flag per
-                                          // workgroup-range boundary (zeroed once, never reset)
+  DevBuf split_ws, split_cnt;             // split GEMM last-round K-split: chunk slabs and a
+                                          // ticket counter per tile (zeroed once, reset by use)
   hipStream_t st = nullptr;               // (split sub-batches only; the first runs unsplit
   hipEvent_t done = nullptr;              //  batches on the caller's stream)
   void release() {
-    DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot, &sk_ws, &sk_sync};
+    DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot, &split_ws, &split_cnt};
     for (DevBuf* d : b) d->release();
   }
 };
@@ -79,11 +80,11 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // forces the scalar LayerNorm kernels (used for widths the vectorised ones do not cover);
 // HCRAG_ENC_NO_WS keeps the fast modes' QKV / FFN1 projections on gemm_v4 (A/B of gemm_ws).
 // HCRAG_ENC_PADDED runs every token position, padding included (A/B and parity of the packing).
-// HCRAG_SPLIT_SK=1: the split GEMM's stream-K completion (off by default: r04n/r04o measured it
-// slower than whole-tile rounds at bge-base's token counts -- see launch_gemm_split).
+// HCRAG_SPLIT_NONE=1: the split GEMM in whole-tile rounds only (no K-split of the last round;
+// A/B and bit-identity tests of the other paths).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  split_sk = false, sk_diag = false; int streams = 0; };
+                  no_split = false; int streams = 0; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -93,8 +94,7 @@ static const EncHooks& enc_hooks() {
     t.gelu_liberf = getenv("HCRAG_GELU_LIBERF") != nullptr;
     t.no_ws = getenv("HCRAG_ENC_NO_WS") != nullptr;
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
-    t.split_sk = getenv("HCRAG_SPLIT_SK") != nullptr;
-    t.sk_diag = getenv("HCRAG_SK_DIAG") != nullptr;   // timing only: cut tiles' halves never meet
+    t.no_split = getenv("HCRAG_SPLIT_NONE") != nullptr;
     if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
     return t;
   }();
@@ -364,48 +364,46 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 // whole number of 256- or 192-feature tiles), T padded to 256.
 //
 // Decomposition: whole 256- or 192-feature x 256-token tiles in rounds of one workgroup per CU
-// (the LDS ring holds one per CU).  A stream-K completion is built (HCRAG_SPLIT_SK=1): all but
-// the last two rounds' worth of tiles whole, then the remaining tiles' K steps split evenly over
-// one workgroup per CU, cut tiles' halves meeting through a workspace slot (gemm_split_kernel).
-// It balances the rounds (bge-base O / FFN2 at 96 token tiles: 1.125 tile-times per CU instead
-// of 2 rounds) but measured slower overall (r04n kernel traces, one box, 96 / 97 token tiles):
-// O / FFN2 236 vs 259 us at 96 but 263 vs 258 at 97, FFN1 347-361 vs 332-335, QKV 250-263 vs
-// 240-244, and the attention after a stream-K QKV 86 vs 78 us.  Workgroups that share a token
-// tile's activations run at different K offsets in the split ranges, so the activations are
-// fetched once per workgroup instead of once per round from L2, and the cut tiles' slabs (256
-// KiB each, read back in a burst at the launch's end) cost ~12 us per GEMM.  Default off.
-struct SplitPlan { int ft, nft, grid, dp_tiles, sk_iters; };
-static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool sk) {
+// (the LDS ring holds one per CU), then the R tiles of a partly filled last round split into s
+// K-chunks each (s = ncu / R, <= 8, one round; gemm_split_kernel<SPLIT>).  The width and the
+// split are chosen by estimated time: tile-times per CU (a 192-wide tile costs 0.86 of a 256
+// one: r04n whole-tile traces, 51.8 vs 60 us at K = 768; r02: 0.86) plus the split launch's
+// overhead over its chunks' MFMA time (slab stores, the last arriver reading s 256-KiB slabs:
+// ~9 + 4.3 s us, r04q traces: 17 us at s = 2, 43 at s = 8).  Measured (r04q, one box, A/B):
+// f32 encoder 67.1k -> 69.8k embeddings/s, f32 query pipeline 36.1k -> 36.7k queries/s.
+// Stream-K over a linear (tile, k) order was built
+// first and measured neutral to negative (r04n/r04o): its split ranges put the
+// workgroups that share a token tile's activations at different K offsets.
+struct SplitPlan { int ft, nft, full, rem, nsplit; };
+static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool split_on) {
   const int ntt = (int)(rup(T, G4_T) / G4_T);
-  auto tiles = [&](int ft) { return (int)(rup(N, ft) / ft) * ntt; };
-  bool use192;
-  if (force_ft) {
-    use192 = force_ft == 192;
-  } else if (sk && tiles(256) > ncu) {
-    // stream-K: tile-times per CU.  A 192-wide tile measured 0.75 of a 256 one (r04f, bge-base
-    // T = 24.6k, whole-tile rounds: 53 vs 71 us at K = 768), so the two widths balance alike;
-    // the stream-K kernel keeps its registers at 192 (252 VGPRs, no spills) and spills at 256
-    // (256 VGPRs, 70-95 scratch accesses around the epilogue in its segment loop)
-    use192 = true;
-  } else {
-    // whole-tile rounds: a round of 192-wide tiles cost ~0.86 of a 256 one (r02, T = 32768:
-    // QKV 6 rounds 354 us vs 5 rounds 344 us; O / FFN2 295 vs 337 us; profiles/r02/encoder_split/)
-    auto rounds = [&](int ft) { return (double)((tiles(ft) + ncu - 1) / ncu); };
-    use192 = rounds(192) * 0.86 < rounds(256);
+  const int nsteps = K / V3_BK;
+  const double t256 = 60.0 * K / 768.0;                  // us per 256-wide tile round
+  SplitPlan best{};
+  double best_us = 1e30;
+  // (a forced width the epilogue cannot take -- 192 for FFN1 -- falls back to 256)
+  const int forced = (force_ft == 192 && !can192) ? G4_T : force_ft;
+  for (int ft : {192, G4_T}) {
+    if (ft == 192 && !can192) continue;
+    if (forced && ft != forced) continue;
+    SplitPlan p{};
+    p.ft = ft;
+    p.nft = (int)(rup(N, ft) / ft);
+    const int nt = p.nft * ntt;
+    p.full = nt / ncu * ncu;
+    p.rem = nt - p.full;
+    p.nsplit = p.rem ? std::min({ncu / p.rem, nsteps, 8}) : 0;
+    const double w = ft == 192 ? 0.86 : 1.0;
+    double us;
+    if (!split_on || p.nsplit < 2) {
+      p.full = nt; p.rem = 0; p.nsplit = 0;
+      us = (double)((nt + ncu - 1) / ncu) * w * t256;
+    } else {
+      us = ((double)(p.full / ncu) + 1.0 / p.nsplit) * w * t256 + 9.0 + 4.3 * p.nsplit;
+    }
+    if (us < best_us) { best_us = us; best = p; }
   }
-  SplitPlan p{};
-  p.ft = can192 && use192 ? 192 : G4_T;
-  p.nft = (int)(rup(N, p.ft) / p.ft);
-  const int nt = p.nft * ntt;
-  if (!sk || nt <= ncu || nt % ncu == 0) {
-    p.grid = nt; p.dp_tiles = nt; p.sk_iters = 0;
-  } else {
-    // every stream-K range >= one tile's K steps: a tile is cut at most once
-    p.grid = ncu;
-    p.dp_tiles = (nt / ncu - 1) * ncu;
-    p.sk_iters = (nt - p.dp_tiles) * (K / V3_BK);
-  }
-  return p;
+  return best;
 }
 
 template <int EPI>
@@ -416,23 +414,23 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
   if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
   // (FFN1's epilogue stages 64-feature halves: 256-feature tiles only)
   constexpr bool can192 = EPI != EPI_BIAS_GELU_SPLIT;
-  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, enc_hooks().split_sk);
+  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, !enc_hooks().no_split);
   float* ws = nullptr;
-  uint32_t* sync = nullptr;
-  if (p.sk_iters) {
-    CHECK(w.sk_ws.ensure((size_t)ncu * G4_T * G4_T * 4));
-    CHECK(w.sk_sync.ensure((size_t)ncu * 2 * 4));
-    ws = w.sk_ws.as<float>();
-    sync = enc_hooks().sk_diag ? nullptr : w.sk_sync.as<uint32_t>();
+  uint32_t* cnt = nullptr;
+  if (p.nsplit) {
+    // s slabs of a tile's fp32 accumulators per remainder tile (rem x nsplit <= ncu), a counter each
+    CHECK(w.split_ws.ensure((size_t)ncu * G4_T * G4_T * 4));
+    CHECK(w.split_cnt.ensure((size_t)ncu * 4));
+    ws = w.split_ws.as<float>();
+    cnt = w.split_cnt.as<uint32_t>();
   }
-  // the data-parallel rounds (whole tiles), then the stream-K launch over the rest
-#define HCR_SPLIT(FT_, LIB_, SK_, GRID_, BASE_)                                                    \
-  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_, SK_>), dim3((unsigned)(GRID_)), dim3(V3_NT), 0, st, \
-                     W, X, K, N, T, p.nft, bias, resid, out_h, out_f, ldo, oscale, BASE_, p.sk_iters, ws, sync)
+#define HCR_SPLIT(FT_, LIB_, SP_, GRID_)                                                            \
+  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_, SP_>), dim3((unsigned)(GRID_)), dim3(V3_NT), 0, st, \
+                     W, X, K, N, T, p.nft, bias, resid, out_h, out_f, ldo, oscale, p.full, p.nsplit, ws, cnt)
 #define HCR_SPLIT_FT(FT_, LIB_)                                                                     \
   do {                                                                                              \
-    if (p.dp_tiles > 0) HCR_SPLIT(FT_, LIB_, false, p.dp_tiles, 0);                                 \
-    if (p.sk_iters > 0) HCR_SPLIT(FT_, LIB_, true, p.grid, p.dp_tiles);                             \
+    if (p.full > 0) HCR_SPLIT(FT_, LIB_, false, p.full);                                            \
+    if (p.nsplit > 0) HCR_SPLIT(FT_, LIB_, true, p.rem * p.nsplit);                                 \
   } while (0)
   if constexpr (!can192) {
     if (enc_hooks().gelu_liberf) HCR_SPLIT_FT(G4_T, true);

@@ -339,99 +339,92 @@ __device__ __forceinline__ void g5_read6(uint32_t a, half8 (&av)[6]) {
       : "memory");
 }
 
-// Stream-K completion of the split GEMM (the reference-precision mode's wave quantization: at
-// bge-base T ~ 24.6k packed tokens O-proj / FFN2 are 388 192-wide or 291 256-wide tiles -- 2
-// rounds of 256 resident workgroups, the second 13-52 % full).  A launch of G workgroups runs
-// dp_tiles whole tiles (g, g + G, ...) and then splits the remaining tiles' K steps evenly:
-// workgroup g takes steps [g S / G, (g + 1) S / G) of that range (S = sk_iters).  Each range is
-// at least one tile long, so a tile is cut at most once, at a range boundary b, into a head
-// (steps from 0; the end of range b - 1) and a tail (the start of range b).  The two halves meet
-// through slot b of the workspace: the first to draw a ticket publishes its fp32 accumulators
-// (write-through stores, then an agent-scope flag), the second waits for that flag -- only ever
-// for a workgroup that is already running, so no residency is assumed -- adds the slab and runs
-// the epilogue.  a + b = b + a: the result does not depend on which half arrives first.
-// Counters and flags are never reset: each slot gets 0 or 2 tickets per launch, so ticket >> 1
-// numbers the launches that used it and (ticket >> 1) + 1 is the epoch its flag carries.
+// Split of the last round (the reference-precision mode's wave quantization: at bge-base T ~
+// 24.6k packed tokens O-proj / FFN2 are 384 192-wide tiles -- a full round of 256 CUs and a
+// second of 128 -- and QKV / FFN1 1152: 4 rounds and a half).  The R tiles left after the full
+// rounds run as s K-chunks each (s = ncu / R, at most 8), one workgroup per chunk, all in one
+// round: chunk c of a tile takes K steps [c n / s, (c + 1) n / s).  The chunks of every tile
+// run at the same time, so workgroups that share a token tile's activations read each K chunk
+// of them together (one fetch from HBM, the rest from L2) -- what a stream-K split over a
+// linear (tile, k) order lost (r04n).  Every chunk stores its fp32 accumulators to the tile's
+// slab c (write-through), drains, and draws a ticket; the tile's last arriver sums slabs 0 ..
+// s-1 in that order (the result does not depend on the arrival order) and runs the epilogue,
+// and resets the counter for the next launch (zeroed once when allocated).  No workgroup waits
+// for another: no residency is assumed.
 typedef __attribute__((address_space(1))) uint32_t sk_gu32;
 typedef uint32_t uint32x4 __attribute__((ext_vector_type(4)));
 
+// slab image: the accumulators in register order, float4 (wave, m, n) per lane -- 1 KiB per
+// instruction per wave both ways.  Returns true in the tile's last arriving workgroup, with acc
+// = the sum of the tile's s chunks (in chunk order).
 template <int MT>
-__device__ __forceinline__ bool sk_meet(floatx4 (&acc)[MT][4], char* ring, float* slab_base,
-                                        uint32_t* sync, int slot, int nslots, int tid) {
+__device__ __forceinline__ bool split_gather(floatx4 (&acc)[MT][4], char* ring, float* slabs, uint32_t* cnt,
+                                             int chunk, int s, int tid) {
   constexpr int NQ = 4;
+  constexpr int SLAB = MT * NQ * 256 * 8;          // floats per slab (8 waves)
   const int lane = tid & 63, wave = tid >> 6;
-  sk_gu32* cnt = (sk_gu32*)sync + slot;
-  sk_gu32* flag = (sk_gu32*)sync + nslots + slot;
-  __syncthreads();                                   // every wave out of the main loop's LDS
+  float* mine = slabs + (size_t)chunk * SLAB + (size_t)wave * (MT * NQ * 256);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<char*>(mine)), (short)0, MT * NQ * 1024, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+      const floatx4 v = acc[m][n];
+      __builtin_amdgcn_raw_buffer_store_b128(
+          uint32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])},
+          rs, ((m * NQ + n) * 64 + lane) * 16, 0, 16 /* sc1: write-through */);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();                                   // (and every wave is out of the ring)
   if (tid == 0)
-    *reinterpret_cast<uint32_t*>(ring) = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *reinterpret_cast<uint32_t*>(ring) = __hip_atomic_fetch_add((sk_gu32*)cnt, 1u, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const uint32_t ticket = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(ring));
-  const uint32_t epoch = (ticket >> 1) + 1u;
-  // slab image: the accumulators in register order, float4 (wave, m, n) per lane -- 1 KiB per
-  // instruction per wave, both ways
-  float* slab = slab_base + (size_t)wave * (MT * NQ * 256);
-  if ((ticket & 1u) == 0u) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(reinterpret_cast<char*>(slab)), (short)0, MT * NQ * 1024, 0x00020000);
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) {
-        const floatx4 v = acc[m][n];
-        __builtin_amdgcn_raw_buffer_store_b128(
-            uint32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])},
-            rs, ((m * NQ + n) * 64 + lane) * 16, 0, 16 /* sc1: write-through */);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-  }
-  if (tid == 0) {
-    // bounded: the publisher holds a ticket, so it is running; the bound only turns a protocol
-    // bug into wrong numbers instead of a hung queue
-    for (uint32_t spins = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch &&
-                             spins < (1u << 22); ++spins)
-      __builtin_amdgcn_s_sleep(2);
-  }
-  __syncthreads();
-  // every slab byte was stored write-through (sc1) and drained before the flag, and every load
-  // of it below is an sc1 load (past this CU's L1): no agent-scope acquire needed, only the
-  // compiler kept from hoisting the loads above the poll
+  if (ticket != (uint32_t)(s - 1)) return false;
+  if (tid == 0) __hip_atomic_store((sk_gu32*)cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // every slab byte was stored write-through (sc1) and drained before its ticket, and every load
+  // of it below is an sc1 load (past this CU's L1): no agent-scope acquire, only the compiler
+  // kept from hoisting the loads above the ticket
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const float* src = slab + lane * 4;
+  const float* base = slabs + (size_t)wave * (MT * NQ * 256) + lane * 4;
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    floatx4 p0, p1, p2, p3;
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off sc1\n\t"
-        "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
-        "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
-        "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
-        "s_waitcnt vmcnt(0)"
-        : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3)
-        : "v"(src + m * NQ * 256)
-        : "memory");
-    acc[m][0] += p0; acc[m][1] += p1; acc[m][2] += p2; acc[m][3] += p3;
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int c = 0; c < s; ++c) {
+    const float* src = base + (size_t)c * SLAB;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      floatx4 p0, p1, p2, p3;
+      asm volatile(
+          "global_load_dwordx4 %0, %4, off sc1\n\t"
+          "global_load_dwordx4 %1, %4, off offset:1024 sc1\n\t"
+          "global_load_dwordx4 %2, %4, off offset:2048 sc1\n\t"
+          "global_load_dwordx4 %3, %4, off offset:3072 sc1\n\t"
+          "s_waitcnt vmcnt(0)"
+          : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3)
+          : "v"(src + m * NQ * 256)
+          : "memory");
+      acc[m][0] += p0; acc[m][1] += p1; acc[m][2] += p2; acc[m][3] += p3;
+    }
   }
   return true;
 }
 
 // LIBERF: the FFN1 epilogue's GELU with the library erff (~50 instructions) instead of erf_as
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
-// SK = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index), the
-// data-parallel rounds; SK = true: the stream-K launch over tiles tile_base.. (sk_iters K steps
-// split evenly over the grid).  Two instantiations rather than one loop over both: the loop
-// around the epilogue cost the data-parallel tiles 12-16 % (256 VGPRs and spills against 191 and
-// none: r04m/r04n traces).
-template <int EPI, int FT = G4_T, bool LIBERF = false, bool SK = false>
+// SPLIT = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index);
+// SPLIT = true: workgroup g is chunk g % nsplit of tile tile_base + g / nsplit (see above).
+template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
                   const float* __restrict__ resid, _Float16* __restrict__ out_h,
-                  float* __restrict__ out_f, int ldo, float oscale, int tile_base, int sk_iters,
-                  float* __restrict__ sk_ws, uint32_t* __restrict__ sk_sync) {
+                  float* __restrict__ out_f, int ldo, float oscale, int tile_base, int nsplit,
+                  float* __restrict__ split_ws, uint32_t* __restrict__ split_cnt) {
   using Op = MfmaOp<_Float16>;
   using V = half8;
   static_assert(FT == 256 || FT == 192, "feature tile");
@@ -450,191 +443,175 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
   const int nsteps = K / V3_BK;
-  const int sk_hi = SK ? (int)((int64_t)(g + 1) * sk_iters / nwg) : 0;
-  int pos = SK ? (int)((int64_t)g * sk_iters / nwg) : 0;
+  int tile = g, ks0 = 0, ks1 = nsteps, chunk = 0;
+  if constexpr (SPLIT) {
+    const int t = g / nsplit;
+    chunk = g - t * nsplit;
+    tile = tile_base + t;
+    ks0 = chunk * nsteps / nsplit;
+    ks1 = (chunk + 1) * nsteps / nsplit;
+  }
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  ks0 = __builtin_amdgcn_readfirstlane(ks0);
+  ks1 = __builtin_amdgcn_readfirstlane(ks1);
+  const int ft = tile % n_tiles_feat, tt = tile / n_tiles_feat;
+  const int f0 = ft * FT, t0 = tt * G4_T;
 
   const int ldb = 3 * K * 2;                   // bytes per split row
   const int drow = lane >> 2;
   const int dchunk = (lane & 3) ^ (int)((V3_SWZ >> (((lane >> 4) & 3) * 4)) & 3u);
   const int voff = drow * ldb + dchunk * 16;
+  const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, FT * ldb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(reinterpret_cast<const char*>(X) + (size_t)t0 * ldb), (short)0, G4_T * ldb, 0x00020000);
   const __amdgpu_buffer_rsrc_t w_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(W), (short)0, 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t x_null = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(X), (short)0, 0, 0x00020000);
+
+  // piece i (0 .. PPW-1) of this wave for stage `is`.  FT = 256: region i / 2 (Wh, Wl', Xh,
+  // Xl'), 16-row block wave + 8 (i % 2).  FT = 192: i = 0 Wh block wave; i = 1 Wh block 8 +
+  // wave (waves 0-3) or Wl block wave - 4 (waves 4-7: same W descriptor, a wave-uniform
+  // choice of offsets); i = 2 Wl block 4 + wave; i = 3, 4 Xh; i = 5, 6 Xl.  The segment of the
+  // split rows: Wh = 2, Wl' = 1, Xh = 0, Xl' = 2.
+  auto issue_piece = [&](int is, int i) __attribute__((always_inline)) {
+    const bool live = is < ks1;
+    const int kofs = __builtin_amdgcn_readfirstlane(is * (V3_BK * 2));
+    char* sa = ring + __builtin_amdgcn_readfirstlane(is & 1) * STAGE;
+    int region, jb;
+    if constexpr (FT == 256) {
+      region = i >> 1;
+      jb = wave + 8 * (i & 1);
+    } else {
+      if (i == 0) { region = 0; jb = wave; }
+      else if (i == 1) { region = wave < 4 ? 0 : 1; jb = wave < 4 ? 8 + wave : wave - 4; }
+      else if (i == 2) { region = 1; jb = 4 + wave; }
+      else { region = 2 + (i - 3) / 2; jb = wave + 8 * ((i - 3) & 1); }
+    }
+    const int seg = region == 0 ? 2 : region == 1 ? 1 : region == 2 ? 0 : 2;
+    const int rbase = region == 0 ? WH : region == 1 ? WL : region == 2 ? XH : XL;
+    if (region < 2)
+      dma16(live ? w_rsrc : w_null, sa + rbase + jb * 1024, voff, jb * 16 * ldb + seg * 2 * K + kofs);
+    else
+      dma16(live ? x_rsrc : x_null, sa + rbase + jb * 1024, voff, jb * 16 * ldb + seg * 2 * K + kofs);
+  };
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) issue_piece(ks0, i);
+
   const int fr = lane & 15, fc = lane >> 4;
   const int fslot = v3_slot(fc, fr);
   const int offA = (wm * (FT / 2) + fr) * 64 + fslot * 16;
   const int offB = (wn * 64 + fr) * 64 + fslot * 16;
-
-  for (int j = 0;; ++j) {
-    // this workgroup's next segment: its whole tile, or the next piece of its K range
-    int tile, ks0, ks1;
-    if constexpr (!SK) {
-      if (j > 0) break;
-      tile = g; ks0 = 0; ks1 = nsteps;
-    } else {
-      if (pos >= sk_hi) break;
-      const int u = pos / nsteps;
-      tile = tile_base + u;
-      ks0 = pos - u * nsteps;
-      ks1 = min(nsteps, ks0 + (sk_hi - pos));
-      pos += ks1 - ks0;
-    }
-    tile = __builtin_amdgcn_readfirstlane(tile);
-    ks0 = __builtin_amdgcn_readfirstlane(ks0);
-    ks1 = __builtin_amdgcn_readfirstlane(ks1);
-    const int ft = tile % n_tiles_feat, tt = tile / n_tiles_feat;
-    const int f0 = ft * FT, t0 = tt * G4_T;
-    const __amdgpu_buffer_rsrc_t w_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(reinterpret_cast<const char*>(W) + (size_t)f0 * ldb), (short)0, FT * ldb, 0x00020000);
-    const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        uniform_ptr(reinterpret_cast<const char*>(X) + (size_t)t0 * ldb), (short)0, G4_T * ldb, 0x00020000);
-
-    // piece i (0 .. PPW-1) of this wave for stage `is`.  FT = 256: region i / 2 (Wh, Wl', Xh,
-    // Xl'), 16-row block wave + 8 (i % 2).  FT = 192: i = 0 Wh block wave; i = 1 Wh block 8 +
-    // wave (waves 0-3) or Wl block wave - 4 (waves 4-7: same W descriptor, a wave-uniform
-    // choice of offsets); i = 2 Wl block 4 + wave; i = 3, 4 Xh; i = 5, 6 Xl.  The segment of the
-    // split rows: Wh = 2, Wl' = 1, Xh = 0, Xl' = 2.
-    auto issue_piece = [&](int is, int i) __attribute__((always_inline)) {
-      const bool live = is < ks1;
-      const int kofs = __builtin_amdgcn_readfirstlane(is * (V3_BK * 2));
-      char* sa = ring + __builtin_amdgcn_readfirstlane(is & 1) * STAGE;
-      int region, jb;
-      if constexpr (FT == 256) {
-        region = i >> 1;
-        jb = wave + 8 * (i & 1);
-      } else {
-        if (i == 0) { region = 0; jb = wave; }
-        else if (i == 1) { region = wave < 4 ? 0 : 1; jb = wave < 4 ? 8 + wave : wave - 4; }
-        else if (i == 2) { region = 1; jb = 4 + wave; }
-        else { region = 2 + (i - 3) / 2; jb = wave + 8 * ((i - 3) & 1); }
-      }
-      const int seg = region == 0 ? 2 : region == 1 ? 1 : region == 2 ? 0 : 2;
-      const int rbase = region == 0 ? WH : region == 1 ? WL : region == 2 ? XH : XL;
-      if (region < 2)
-        dma16(live ? w_rsrc : w_null, sa + rbase + jb * 1024, voff, jb * 16 * ldb + seg * 2 * K + kofs);
-      else
-        dma16(live ? x_rsrc : x_null, sa + rbase + jb * 1024, voff, jb * 16 * ldb + seg * 2 * K + kofs);
-    };
-    __syncthreads();                 // the previous segment's epilogue is done with the ring
+  floatx4 acc[MT][NQ];
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) issue_piece(ks0, i);
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    floatx4 acc[MT][NQ];
+  for (int s = ks0; s < ks1; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
+    const char* st = ring + (s & 1) * STAGE;
+    V av[MT], bq[NQ], bl[NQ];
+    if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
+    else g5_read6(lds_addr(st + WH + offA), av);
+    g5_read4(lds_addr(st + XL + offB), bl);
+    g5_read4(lds_addr(st + XH + offB), bq);
+    // Xl' . Wh
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+    issue_piece(s + 1, 0);
+    issue_piece(s + 1, 1);
+    issue_piece(s + 1, 2);
+    // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+    issue_piece(s + 1, 3);
+    issue_piece(s + 1, 4);
+    issue_piece(s + 1, 5);
+    // Xh . Wl'
+    if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
+    else g5_read6(lds_addr(st + WL + offA), av);
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+    issue_piece(s + 1, 6);
+    if constexpr (PPW == 8) issue_piece(s + 1, 7);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-    for (int s = ks0; s < ks1; ++s) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
-      const char* st = ring + (s & 1) * STAGE;
-      V av[MT], bq[NQ], bl[NQ];
-      if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
-      else g5_read6(lds_addr(st + WH + offA), av);
-      g5_read4(lds_addr(st + XL + offB), bl);
-      g5_read4(lds_addr(st + XH + offB), bq);
-      // Xl' . Wh
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-      issue_piece(s + 1, 0);
-      issue_piece(s + 1, 1);
-      issue_piece(s + 1, 2);
-      // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-      issue_piece(s + 1, 3);
-      issue_piece(s + 1, 4);
-      issue_piece(s + 1, 5);
-      // Xh . Wl'
-      if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
-      else g5_read6(lds_addr(st + WL + offA), av);
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-      issue_piece(s + 1, 6);
-      if constexpr (PPW == 8) issue_piece(s + 1, 7);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (SPLIT) {
+    const int slot = tile - tile_base;
+    if (!split_gather<MT>(acc, ring, split_ws + (size_t)slot * nsplit * (MT * NQ * 256 * 8),
+                          split_cnt + slot, chunk, nsplit, tid))
+      return;
+  }
 
-    if constexpr (SK) {
-      if (ks0 > 0 || ks1 < nsteps) {
-        // a cut tile: slot = the range boundary inside it (this range's start or end)
-        const int slot = ks0 > 0 ? g : g + 1;
-        if (!sk_sync) {                 // (timing diagnostic HCRAG_SK_DIAG=1: no meeting, wrong sums)
-          if (ks0 > 0) continue;
-        } else if (!sk_meet<MT>(acc, ring, sk_ws + (size_t)slot * (FT * G4_T), sk_sync, slot, nwg, tid)) {
-          continue;
+  if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
+    static_assert(FT == 256, "the FFN1 epilogue stages 64-feature halves of a 128-feature wave");
+    // FFN1: the split activations (h, l) go out through LDS.  Stored straight from the
+    // accumulators a lane writes 4 features of one token: 32-B pieces of 16 different rows per
+    // instruction, half-line writes on ~400 MB per launch.  Here each wave stages 64 features x
+    // 64 tokens of h and of l (8 KiB each, 16-B granules XOR-swizzled by token) in its 16 KiB of
+    // the now idle ring, then writes 128-B row pieces: 8 lanes per token row.
+    __syncthreads();                               // every wave done with the ring
+    char* hs = ring + wave * 16384;
+    char* ls = hs + 8192;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int m = hh * 4 + mi;
+        const int fl = mi * 16 + (lane >> 4) * 4;               // feature within the 64
+        const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * 128 + hh * 64 + fl);
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+          const int tl = n * 16 + (lane & 15);                  // token within the 64
+          float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                        fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+          union { _Float16 e[4]; uint2 u; } ph, pl;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = LIBERF ? gelu_exact(v[r]) : gelu_erf(v[r]);
+            ph.e[r] = (_Float16)v[r];
+            pl.e[r] = (_Float16)((v[r] - (float)ph.e[r]) * kSplitLo);
+          }
+          const int off = tl * 128 + (((fl >> 3) ^ (tl & 7)) << 4) + (fl & 7) * 2;
+          *reinterpret_cast<uint2*>(hs + off) = ph.u;
+          *reinterpret_cast<uint2*>(ls + off) = pl.u;
         }
       }
-    }
-
-    if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
-      static_assert(FT == 256, "the FFN1 epilogue stages 64-feature halves of a 128-feature wave");
-      // FFN1: the split activations (h, l) go out through LDS.  Stored straight from the
-      // accumulators a lane writes 4 features of one token: 32-B pieces of 16 different rows per
-      // instruction, half-line writes on ~400 MB per launch.  Here each wave stages 64 features x
-      // 64 tokens of h and of l (8 KiB each, 16-B granules XOR-swizzled by token) in its 16 KiB of
-      // the now idle ring, then writes 128-B row pieces: 8 lanes per token row.
-      __syncthreads();                               // every wave done with the ring
-      char* hs = ring + wave * 16384;
-      char* ls = hs + 8192;
+      wave_lds_sync();
+      // 64 rows x 8 granules: 8 rows per instruction, lane -> (row lane / 8, granule lane % 8)
+      const int gr = lane & 7;
+      const int fcol = f0 + wm * 128 + hh * 64 + gr * 8;
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const int m = hh * 4 + mi;
-          const int fl = mi * 16 + (lane >> 4) * 4;               // feature within the 64
-          const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * 128 + hh * 64 + fl);
-#pragma unroll
-          for (int n = 0; n < NQ; ++n) {
-            const int tl = n * 16 + (lane & 15);                  // token within the 64
-            float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
-                          fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
-            union { _Float16 e[4]; uint2 u; } ph, pl;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              v[r] = LIBERF ? gelu_exact(v[r]) : gelu_erf(v[r]);
-              ph.e[r] = (_Float16)v[r];
-              pl.e[r] = (_Float16)((v[r] - (float)ph.e[r]) * kSplitLo);
-            }
-            const int off = tl * 128 + (((fl >> 3) ^ (tl & 7)) << 4) + (fl & 7) * 2;
-            *reinterpret_cast<uint2*>(hs + off) = ph.u;
-            *reinterpret_cast<uint2*>(ls + off) = pl.u;
-          }
+      for (int i = 0; i < 8; ++i) {
+        const int tl = i * 8 + (lane >> 3);
+        const int t = t0 + wn * 64 + tl;
+        const int off = tl * 128 + ((gr ^ (tl & 7)) << 4);
+        const uint4 h4 = *reinterpret_cast<const uint4*>(hs + off);
+        const uint4 l4 = *reinterpret_cast<const uint4*>(ls + off);
+        if (t < T_real && fcol < N_real) {
+          _Float16* row = out_h + (size_t)t * 3 * ldo;
+          *reinterpret_cast<uint4*>(row + fcol) = h4;
+          *reinterpret_cast<uint4*>(row + 2 * ldo + fcol) = l4;
         }
-        wave_lds_sync();
-        // 64 rows x 8 granules: 8 rows per instruction, lane -> (row lane / 8, granule lane % 8)
-        const int gr = lane & 7;
-        const int fcol = f0 + wm * 128 + hh * 64 + gr * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int tl = i * 8 + (lane >> 3);
-          const int t = t0 + wn * 64 + tl;
-          const int off = tl * 128 + ((gr ^ (tl & 7)) << 4);
-          const uint4 h4 = *reinterpret_cast<const uint4*>(hs + off);
-          const uint4 l4 = *reinterpret_cast<const uint4*>(ls + off);
-          if (t < T_real && fcol < N_real) {
-            _Float16* row = out_h + (size_t)t * 3 * ldo;
-            *reinterpret_cast<uint4*>(row + fcol) = h4;
-            *reinterpret_cast<uint4*>(row + 2 * ldo + fcol) = l4;
-          }
-        }
-        wave_lds_sync();
       }
-    } else {
-      // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well
-      static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
-      __syncthreads();                               // every wave done with the ring
-      staged_epilogue_f32<EPI, MT>(ring + wave * 8192, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64,
-                                   N_real, T_real, bias, resid, out_f, ldo, oscale);
+      wave_lds_sync();
     }
+  } else {
+    // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
+    __syncthreads();                               // every wave done with the ring
+    staged_epilogue_f32<EPI, MT>(ring + wave * 8192, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64,
+                                 N_real, T_real, bias, resid, out_f, ldo, oscale);
   }
 }
 

@@ -350,7 +350,10 @@ def test_packed_tokens_bit_identical_to_padded(tmp_path, dtype, pool, shape):
     """Token packing (pack_tokens_kernel: only tokens with mask 1 -- plus a CLS row -- run through
     the layers) against the padded path (HCRAG_ENC_PADDED=1, in a child process: the hook is read
     once per process): with right padding every kept token sees the same keys in the same order
-    and every row-wise kernel computes the same row, so the embeddings are bit-identical."""
+    and every row-wise kernel computes the same row, so the embeddings are bit-identical.  (The
+    reference-precision GEMM splits a partly filled last round into K-chunks sized by the token
+    count -- test_split_gemm_last_round -- so both arms run whole-tile rounds here:
+    HCRAG_SPLIT_NONE=1.)"""
     import json
     import os
     import subprocess
@@ -370,8 +373,11 @@ def test_packed_tokens_bit_identical_to_padded(tmp_path, dtype, pool, shape):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = str(tmp_path / "padded.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, out],
-                   env=dict(os.environ, HCRAG_ENC_PADDED="1"), check=True, timeout=240)
-    np.testing.assert_array_equal(got, np.load(out))
+                   env=dict(os.environ, HCRAG_ENC_PADDED="1", HCRAG_SPLIT_NONE="1"), check=True, timeout=240)
+    packed = str(tmp_path / "packed.npy")
+    subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, packed],
+                   env=dict(os.environ, HCRAG_SPLIT_NONE="1"), check=True, timeout=240)
+    np.testing.assert_array_equal(np.load(packed), np.load(out))
     _check(got, _ref_embed(m, ids, mask, pool), dtype)
 
 
@@ -424,42 +430,34 @@ def test_two_stream_split_bit_identical(tmp_path, dtype, monkeypatch):
     np.savez(inp, ids=ids, mask=mask, dtype=dtype, cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # the f32 mode's GEMM splits a partly filled last round by each stream's token count
+    # (test_split_gemm_last_round): the bit comparison runs on whole-tile rounds
+    whole = {"HCRAG_SPLIT_NONE": "1"} if dtype == "f32" else {}
     one = str(tmp_path / "one.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, one],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="1"), check=True, timeout=240)
-    np.testing.assert_array_equal(got, np.load(one))
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="1", **whole), check=True, timeout=240)
     two = str(tmp_path / "two.npy")
     subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, two],
-                   env=dict(os.environ, HCRAG_ENC_STREAMS="2"), check=True, timeout=240)
-    np.testing.assert_array_equal(got, np.load(two))
+                   env=dict(os.environ, HCRAG_ENC_STREAMS="2", **whole), check=True, timeout=240)
+    np.testing.assert_array_equal(np.load(one), np.load(two))
+    if dtype == "f32":
+        assert np.abs(got - np.load(one)).max() <= 1e-5
+    else:
+        np.testing.assert_array_equal(got, np.load(one))
     _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
 
 
-_SK_CHILD = r"""
-import sys, numpy as np
-sys.path[:0] = [sys.argv[1], sys.argv[2]]
-d = np.load(sys.argv[3])
-from hcrag_amd import BertEncoder
-import json
-cfg = json.loads(str(d["cfg"]))
-state = {k[3:]: d[k] for k in d.files if k.startswith("sd_")}
-enc = BertEncoder(cfg, state, dtype=str(d["dtype"]))
-a = enc.encode_ids(d["ids"], d["mask"])
-b = enc.encode_ids(d["ids"], d["mask"])
-np.save(sys.argv[4], np.stack([a, b]))
-"""
-
-
 @pytest.mark.gpu
-def test_split_gemm_stream_k(tmp_path):
-    """The reference-precision GEMM's stream-K completion (HCRAG_SPLIT_SK=1, off by default:
-    encoder.hip split_plan / launch_gemm_split, gemm_v4.h gemm_split_kernel<SK> / sk_meet): at
-    T ~ 26k packed tokens every bge-base projection has more tiles than compute units and a
-    partly filled last round -- QKV and FFN1 run whole tiles in rounds and then K-split ranges,
-    O / FFN2 K-split ranges only (K = 768: 24 steps, K = 3072: 96).  A cut tile's halves meet
-    through a slot whichever arrives first, so two runs are the same bits; the K split moves the
-    fp32 sums by rounding only, so the embeddings stay within 1e-5 of the whole-tile rounds (the
-    default, in this process) and within the f32 bar of fp32 BertModel."""
+@pytest.mark.parametrize("n", [1100, 60])
+def test_split_gemm_last_round(tmp_path, n):
+    """The reference-precision GEMM's K-split of a partly filled last round (encoder.hip
+    split_plan / launch_gemm_split, gemm_v4.h gemm_split_kernel<SPLIT> / split_gather): at T ~
+    26k packed tokens (n = 1100) bge-base's projections run whole-tile rounds and then their
+    remainder tiles as 2-8 K-chunks each; at n = 60 (~1.5k tokens) every projection has fewer
+    tiles than compute units and runs split only.  The chunks are summed in chunk order by
+    whichever arrives last, so two runs are the same bits; the split moves the fp32 sums by
+    rounding only: within 1e-5 of whole-tile rounds (HCRAG_SPLIT_NONE=1, child process: the
+    hook is read once per process) and within the f32 bar of fp32 BertModel."""
     import json
     import os
     import subprocess
@@ -468,21 +466,21 @@ def test_split_gemm_stream_k(tmp_path):
     cfg = dict(BGE_BASE_2L, num_hidden_layers=3)
     conf, m = _hf_model(cfg, 31)
     rng = np.random.default_rng(31)
-    n, S = 1100, 32
+    S = 32
     ids, mask = _batch(rng, n, S, cfg["vocab_size"], lens=rng.integers(16, S + 1, size=n))
-    assert int(mask.sum()) > 256 * 86           # > 85 token tiles: O / FFN2 have > 256 tiles
     enc = _encoder(conf, m, "f32", pooling="cls")
-    c = enc.encode_ids(ids, mask)
+    a = enc.encode_ids(ids, mask)
+    b = enc.encode_ids(ids, mask)
+    np.testing.assert_array_equal(a, b)
     inp = str(tmp_path / "in.npz")
     np.savez(inp, ids=ids, mask=mask, dtype="f32", cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sk = str(tmp_path / "sk.npy")
-    subprocess.run([sys.executable, "-c", _SK_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, sk],
-                   env=dict(os.environ, HCRAG_SPLIT_SK="1"), check=True, timeout=240)
-    a, b = np.load(sk)
-    np.testing.assert_array_equal(a, b)
+    whole = str(tmp_path / "whole.npy")
+    subprocess.run([sys.executable, "-c", _PADDED_CHILD, root, os.path.join(root, "hc-rag_amd"), inp, whole],
+                   env=dict(os.environ, HCRAG_SPLIT_NONE="1"), check=True, timeout=240)
+    c = np.load(whole)
     d = np.abs(a - c).max()
-    print(f"stream-K vs whole tiles: max |diff| = {d:.3e}")
+    print(f"last-round K-split vs whole tiles: max |diff| = {d:.3e}")
     assert d <= 1e-5, d
     _check(a, _ref_embed(m, ids, mask, "cls"), "f32")
