@@ -639,29 +639,33 @@ attention_f32_mfma_kernel(const float* __restrict__ qkv, const int32_t* __restri
     }
   __syncthreads();
   // O = P.V: output block dt holds columns 4 lr + dt (lanes lr < DH / 4; DH = 32 leaves lanes
-  // 8-15 of each 16 idle in the 16-wide MFMA, their V operand zero)
+  // 8-15 of each 16 idle in the 16-wide MFMA, their V operand zero).  All four blocks are kept,
+  // so a lane stores its 4 consecutive columns of a row as one 8-byte h and one 8-byte l piece
+  // (r04: was 2-byte stores per element, 4x the store instructions; same values)
+  floatx4 o[4][NT];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    floatx4 o[NT];
 #pragma unroll
-    for (int it = 0; it < NT; ++it) o[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < NT; ++it) o[dt][it] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < JI; ++j) {
       const float b = dt == 0 ? vb[j].x : dt == 1 ? vb[j].y : dt == 2 ? vb[j].z : vb[j].w;
 #pragma unroll
       for (int it = 0; it < NT; ++it)
-        o[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ps[(it * 16 + lr) * LP + 4 * j + lk], b, o[it], 0, 0, 0);
+        o[dt][it] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ps[(it * 16 + lr) * LP + 4 * j + lk], b, o[dt][it], 0, 0, 0);
     }
-    if (lr < VL) {
+  }
+  if (lr < VL) {
 #pragma unroll
-      for (int it = 0; it < NT; ++it)
+    for (int it = 0; it < NT; ++it)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = it * 16 + 4 * lk + r;
-          if (i < S)
-            store_act1<_Float16, true>(ctx + (row0 + i) * ld3, H, h * DH + 4 * lr + dt, o[it][r] * inv[it][r]);
-        }
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int i = it * 16 + 4 * lk + r;
+        if (i < S)
+          store_act4<_Float16, true>(ctx + (row0 + i) * ld3, H, h * DH + 4 * lr,
+                                     make_float4(o[0][it][r] * inv[it][r], o[1][it][r] * inv[it][r],
+                                                 o[2][it][r] * inv[it][r], o[3][it][r] * inv[it][r]));
+      }
   }
 }
 
