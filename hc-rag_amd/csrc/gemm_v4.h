@@ -393,8 +393,32 @@ __device__ __forceinline__ bool split_gather(floatx4 (&acc)[MT][4], char* ring, 
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // two slabs' pieces of a row block in flight at a time, added in chunk order
+  int c = 0;
 #pragma unroll 1
-  for (int c = 0; c < s; ++c) {
+  for (; c + 1 < s; c += 2) {
+    const float* src = base + (size_t)c * SLAB;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      floatx4 p0, p1, p2, p3, q0, q1, q2, q3;
+      asm volatile(
+          "global_load_dwordx4 %0, %8, off sc1\n\t"
+          "global_load_dwordx4 %1, %8, off offset:1024 sc1\n\t"
+          "global_load_dwordx4 %2, %8, off offset:2048 sc1\n\t"
+          "global_load_dwordx4 %3, %8, off offset:3072 sc1\n\t"
+          "global_load_dwordx4 %4, %9, off sc1\n\t"
+          "global_load_dwordx4 %5, %9, off offset:1024 sc1\n\t"
+          "global_load_dwordx4 %6, %9, off offset:2048 sc1\n\t"
+          "global_load_dwordx4 %7, %9, off offset:3072 sc1\n\t"
+          "s_waitcnt vmcnt(0)"
+          : "=&v"(p0), "=&v"(p1), "=&v"(p2), "=&v"(p3), "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)
+          : "v"(src + m * NQ * 256), "v"(src + SLAB + m * NQ * 256)
+          : "memory");
+      acc[m][0] += p0; acc[m][1] += p1; acc[m][2] += p2; acc[m][3] += p3;
+      acc[m][0] += q0; acc[m][1] += q1; acc[m][2] += q2; acc[m][3] += q3;
+    }
+  }
+  if (c < s) {
     const float* src = base + (size_t)c * SLAB;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
