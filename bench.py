@@ -270,10 +270,17 @@ class PowerSampler:
         try:
             pr = torch.cuda.get_device_properties(dev_index)
             bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
-            cands = [f"/sys/bus/pci/devices/{bdf}"]
         except Exception:
-            cands = []
-        cands += sorted(glob.glob("/sys/class/drm/card*/device"))
+            bdf = None
+        # only this device's hwmon: the PCI path of its BDF, or a drm card whose
+        # device resolves to that BDF; with no BDF, a card only when the box shows exactly one
+        # (on a shared box any other card may be another job's GPU) -- else 'unknown'
+        drm = sorted(glob.glob("/sys/class/drm/card*/device"))
+        if bdf:
+            cands = [f"/sys/bus/pci/devices/{bdf}"] + [
+                d for d in drm if os.path.basename(os.path.realpath(d)).lower() == bdf.lower()]
+        else:
+            cands = drm if len({os.path.realpath(d) for d in drm}) == 1 else []
         for d in cands:
             hw = sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*")))
             if hw and any(os.path.exists(os.path.join(hw[0], f)) for f in ("power1_average", "power1_input")):

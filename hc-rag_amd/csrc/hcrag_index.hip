@@ -738,7 +738,7 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
   const size_t lds = (size_t)ix->dim * 8 + (size_t)kp * 32 + 16;
   hipLaunchKernelGGL((rescore_kernel<TS>), dim3(nq), dim3(256), lds, st, merged,
                      kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
-                     ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
+                     ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
                      ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
@@ -760,7 +760,7 @@ static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, i
   const int M = next_pow2(std::max(np * kp, kp));
   hipLaunchKernelGGL((finish_kernel<TS>), dim3(nq), dim3(256), finish_lds(np, kp, ix->dim), st, lists, cnt,
                      np, M, kp, d_q, ix->dim, ix->w_qnorm.as<const double>(), ix->w_eps.as<const double>(),
-                     ix->rows.as<const TS>(), ix->ld, ix->norm64.as<const double>(), k, mode, thr,
+                     ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
                      ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
@@ -854,6 +854,14 @@ seed_select_kernel(const float* __restrict__ umax, int U, int nqpad, int nq, int
   if (lane == 0) {
     tau_g[q] = t;
     if (tau_est) tau_est[q] = t;
+  }
+}
+
+// HCRAG_TEST_PLANT_BAD_KEY: slot 0 of query 0's first list := the key (score 2.0, row)
+__global__ void plant_key_kernel(uint64_t* __restrict__ list, int* __restrict__ cnt, uint32_t row) {
+  if (threadIdx.x == 0) {
+    list[0] = ((uint64_t)ord32(2.0f) << 32) | (uint64_t)(0xFFFFFFFFu - row);
+    if (cnt && cnt[0] < 1) cnt[0] = 1;
   }
 }
 
@@ -1107,6 +1115,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int* lcnt = nullptr;
   int lp = 0;
   CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr, &lcnt, &lp));
+  // test hook (read per call, so one process can arm and disarm it): a top-scored key naming
+  // row n + 7 planted into query 0's first list, as a defective score kernel could leave it
+  if (getenv("HCRAG_TEST_PLANT_BAD_KEY")) {
+    hipLaunchKernelGGL(plant_key_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(merged_ptr),
+                       const_cast<int*>(lcnt), (uint32_t)ix->n + 7u);
+    HIPC(hipGetLastError());
+  }
   // fused for small batches (configs[1], B = 256: 0.372 vs 0.376 ms per search); above
   // kFinishMaxQueries the separate launches (W = 8 rank shape, B = 1024: 1.973-1.985 vs
   // 1.985-1.998 ms: the fused block's merge LDS cuts the rescore's residency; r03f A/B)
@@ -1131,9 +1146,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     HIPC(hipGetLastError());
   }
 
-  int cnt = 0;
-  HIPC(hipMemcpyAsync(&cnt, ix->w_cnt.p, 4, hipMemcpyDeviceToHost, st));
+  int cnt2[2] = {0, 0};     // [0] uncertified queries, [1] candidate keys outside the index
+  HIPC(hipMemcpyAsync(cnt2, ix->w_cnt.p, 8, hipMemcpyDeviceToHost, st));
   HIPC(hipStreamSynchronize(st));
+  if (cnt2[1] != 0)
+    return set_err(HCR_EINTERNAL, "internal: a candidate key names a row outside the index (%lld rows); "
+                   "the search was abandoned", (long long)ix->n);
+  const int cnt = cnt2[0];
   *n_unc = cnt;
   if (ix->stats.partitions == 0) {
     ix->stats.partitions = P;
@@ -1331,6 +1350,84 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   return HCR_OK;
 }
 
+// ---- deep top-k: k > kMaxK (the fallback's LDS select holds 8192 slots) ----
+// Every row's exact key per query, sorted per query by a stable segmented radix sort (score
+// desc; rows enter in ascending order, so ties stay row asc), the first k kept.  For the
+// reference's argsort(...)[::-1][:top_k] at any top_k (experiments/main.py:844,889).  Query
+// groups are sized so that keys + rows (in and out) stay within kDeepBudget bytes.
+int hcr_seg_sort_u64_u32(DevBuf& temp, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+                         uint32_t* vout, int num_items, int num_segments, const int* offs,
+                         int descending, hipStream_t st);              // deep_sort.hip
+static constexpr size_t kDeepBudget = (size_t)4 << 30;
+
+__global__ void seg_offsets_kernel(int* __restrict__ offs, int nseg, int len) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= nseg) offs[i] = i * len;
+}
+
+__global__ void deep_out_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                int64_t n, int k, int mode, double thr, int64_t id_offset,
+                                const int64_t* __restrict__ idmap, double* __restrict__ out_s,
+                                int64_t* __restrict__ out_i) {
+  const int q = blockIdx.y;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    double s = -INFINITY;
+    int64_t id = -1;
+    if (t < n) {
+      const uint64_t key = keys[(int64_t)q * n + t];
+      if (key) {
+        double v = unord64(key);
+        if (mode == 1) v = (v + 1.0) / 2.0;
+        if (v >= thr) { s = v; id = row_id(id_offset, idmap, vals[(int64_t)q * n + t]); }
+      }
+    }
+    out_s[(int64_t)q * k + t] = s;
+    out_i[(int64_t)q * k + t] = id;
+  }
+}
+
+static int deep_topk(hcr_index* ix, const float* qc, int m, int k, int mode, double thr, double* os,
+                     int64_t* oi, hipStream_t st) {
+  const int64_t n = ix->n;
+  if (n > INT32_MAX) return set_err(HCR_EINVAL, "k > %d needs an index of < 2^31 rows", kMaxK);
+  int64_t G = std::min<int64_t>(m, std::max<int64_t>(1, (int64_t)(kDeepBudget / ((size_t)n * 24))));
+  G = std::max<int64_t>(1, std::min<int64_t>(G, INT32_MAX / n));
+  DevBuf kin, kout, vin, vout, offs, temp;
+  CHECK(kin.ensure((size_t)G * n * 8));
+  CHECK(kout.ensure((size_t)G * n * 8));
+  CHECK(vin.ensure((size_t)G * n * 4));
+  CHECK(vout.ensure((size_t)G * n * 4));
+  CHECK(offs.ensure((size_t)(G + 1) * 4));
+  CHECK(ix->w_qnorm.ensure((size_t)G * 8));
+  for (int g0 = 0; g0 < m; g0 += (int)G) {
+    const int gm = (int)std::min<int64_t>(G, m - g0);
+    const float* qg = qc + (int64_t)g0 * ix->dim;
+    hipLaunchKernelGGL(query_norms_kernel, dim3((gm + 3) / 4), dim3(256), 0, st, qg, gm, ix->dim,
+                       ix->w_qnorm.as<double>());
+    const dim3 grid((unsigned)((n + 3) / 4), (unsigned)gm);
+    const uint32_t* mb = ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr;
+#define DEEPK(TS)                                                                                  \
+    hipLaunchKernelGGL((deep_keys_kernel<TS>), grid, dim3(256), 0, st, qg, ix->dim,                \
+                       ix->w_qnorm.as<const double>(), ix->rows.as<const TS>(), ix->ld, n,        \
+                       ix->norm64.as<const double>(), mb, kin.as<uint64_t>(), vin.as<uint32_t>())
+    if (ix->dtype == HCR_F16) DEEPK(_Float16); else if (ix->dtype == HCR_BF16) DEEPK(__bf16); else DEEPK(float);
+#undef DEEPK
+    hipLaunchKernelGGL(seg_offsets_kernel, dim3((gm + 256) / 256), dim3(256), 0, st, offs.as<int>(), gm, (int)n);
+    HIPC(hipGetLastError());
+    CHECK(hcr_seg_sort_u64_u32(temp, kin.as<const uint64_t>(), kout.as<uint64_t>(), vin.as<const uint32_t>(),
+                               vout.as<uint32_t>(), (int)(gm * n), gm, offs.as<const int>(), 1, st));
+    const unsigned bx = (unsigned)std::min<int64_t>(1024, (k + 255) / 256);
+    hipLaunchKernelGGL(deep_out_kernel, dim3(bx, (unsigned)gm), dim3(256), 0, st, kout.as<const uint64_t>(),
+                       vout.as<const uint32_t>(), n, k, mode, thr, ix->id_offset,
+                       ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, os + (int64_t)g0 * k,
+                       oi + (int64_t)g0 * k);
+    HIPC(hipGetLastError());
+  }
+  HIPC(hipStreamSynchronize(st));        // (the group buffers are freed on return)
+  return HCR_OK;
+}
+
 // Full search of nq device queries: certified top-k (K1-K4), certificate widening, and the
 // exact fallback for whatever is still uncertified -- every returned list is the exact top-k.
 static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k, int mode,
@@ -1352,6 +1449,11 @@ static int search_device_impl(hcr_index* ix, const float* d_q, int64_t nq, int k
     const float* qc = d_q + q0 * ix->dim;
     double* os = d_out_s + q0 * k;
     int64_t* oi = d_out_i + q0 * k;
+    if (k > kMaxK) {                // deeper than the fallback's select: the sorted full scan
+      CHECK(deep_topk(ix, qc, m, k, mode, thr, os, oi, st));
+      ix->stats.fallback_queries += m;
+      continue;
+    }
     if (k > kMaxFastK) {            // no MFMA candidate path this deep: exact scan
       std::vector<int> all(m);
       for (int i = 0; i < m; ++i) all[i] = i;
@@ -1421,7 +1523,7 @@ extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t 
                                  int64_t* d_out_ids, void* stream) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
-  if (k <= 0 || k > kMaxK) return set_err(HCR_EINVAL, "k must be in [1, %d], got %d", kMaxK, k);
+  if (k <= 0) return set_err(HCR_EINVAL, "k must be >= 1, got %d", k);
   if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
     return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
   if (nq > 0 && (!d_queries || !d_out_scores || !d_out_ids)) return set_err(HCR_EINVAL, "NULL buffer");
@@ -1438,7 +1540,7 @@ extern "C" int hcr_search(hcr_index* ix, const float* queries, int64_t nq, int k
                           double threshold, double* out_scores, int64_t* out_ids) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   if (nq < 0) return set_err(HCR_EINVAL, "negative query count");
-  if (k <= 0 || k > kMaxK) return set_err(HCR_EINVAL, "k must be in [1, %d], got %d", kMaxK, k);
+  if (k <= 0) return set_err(HCR_EINVAL, "k must be >= 1, got %d", k);
   if (score_mode != HCR_SCORE_COSINE && score_mode != HCR_SCORE_UNIT)
     return set_err(HCR_EINVAL, "unknown score_mode %d", score_mode);
   if (nq == 0) return HCR_OK;
@@ -1496,13 +1598,83 @@ extern "C" int hcr_score_all(hcr_index* ix, const float* queries, int64_t nq, in
   return HCR_OK;
 }
 
+// ---- sort-based shard merge (g x k > 8192 keys per query: deeper than K5's LDS sort) ----
+// Two stable segmented radix sorts per query over its g x k entries: by id ascending, then by
+// exact score descending -- (score desc, id asc), the tie rule of K5 -- then the first k.
+__global__ void mrg_id_keys_kernel(const int64_t* __restrict__ ids, int g, int64_t nq, int64_t q0, int nqc,
+                                   int k, uint64_t* __restrict__ keys, uint32_t* __restrict__ pos) {
+  const int64_t gk = (int64_t)g * k;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nqc * gk) return;
+  const int64_t q = i / gk, p = i - q * gk, j = p / k, c = p - j * k;
+  keys[i] = (uint64_t)(ids[(j * nq + q0 + q) * k + c] + 1);    // -1 (empty) -> 0
+  pos[i] = (uint32_t)p;
+}
+__global__ void mrg_score_keys_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g,
+                                      int64_t nq, int64_t q0, int nqc, int k, const uint32_t* __restrict__ pos,
+                                      uint64_t* __restrict__ keys) {
+  const int64_t gk = (int64_t)g * k;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nqc * gk) return;
+  const int64_t q = i / gk, p = pos[i], j = p / k, c = p - j * k;
+  const int64_t off = (j * nq + q0 + q) * k + c;
+  keys[i] = ids[off] >= 0 ? ord64(s[off]) : 0ull;
+}
+__global__ void mrg_out_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g, int64_t nq,
+                               int64_t q0, int nqc, int k, const uint32_t* __restrict__ pos,
+                               double* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  const int64_t gk = (int64_t)g * k;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nqc * k) return;
+  const int64_t q = i / k, t = i - q * k, p = pos[q * gk + t], j = p / k, c = p - j * k;
+  const int64_t off = (j * nq + q0 + q) * k + c;
+  const bool ok = ids[off] >= 0;
+  out_s[(q0 + q) * k + t] = ok ? s[off] : -INFINITY;
+  out_i[(q0 + q) * k + t] = ok ? ids[off] : -1;
+}
+static int merge_sorted(const double* d_scores, const int64_t* d_ids, int g, int64_t nq, int k,
+                        double* d_out_scores, int64_t* d_out_ids, hipStream_t st) {
+  const int64_t gk = (int64_t)g * k;
+  if (gk > INT32_MAX) return set_err(HCR_EINVAL, "g*k must be < 2^31");
+  const int64_t nqc_max = std::max<int64_t>(1, std::min<int64_t>(nq, std::min<int64_t>(INT32_MAX / gk,
+                                                                   (int64_t)(kDeepBudget / (size_t)(gk * 24)))));
+  DevBuf k1, k2, p1, p2, offs, temp;
+  CHECK(k1.ensure((size_t)(nqc_max * gk) * 8));
+  CHECK(k2.ensure((size_t)(nqc_max * gk) * 8));
+  CHECK(p1.ensure((size_t)(nqc_max * gk) * 4));
+  CHECK(p2.ensure((size_t)(nqc_max * gk) * 4));
+  CHECK(offs.ensure((size_t)(nqc_max + 1) * 4));
+  for (int64_t q0 = 0; q0 < nq; q0 += nqc_max) {
+    const int nqc = (int)std::min<int64_t>(nqc_max, nq - q0);
+    const int items = (int)(nqc * gk);
+    const unsigned gr = (unsigned)((items + 255) / 256);
+    hipLaunchKernelGGL(mrg_id_keys_kernel, dim3(gr), dim3(256), 0, st, d_ids, g, nq, q0, nqc, k,
+                       k1.as<uint64_t>(), p1.as<uint32_t>());
+    hipLaunchKernelGGL(seg_offsets_kernel, dim3((nqc + 256) / 256), dim3(256), 0, st, offs.as<int>(), nqc, (int)gk);
+    HIPC(hipGetLastError());
+    CHECK(hcr_seg_sort_u64_u32(temp, k1.as<const uint64_t>(), k2.as<uint64_t>(), p1.as<const uint32_t>(),
+                               p2.as<uint32_t>(), items, nqc, offs.as<const int>(), 0, st));
+    hipLaunchKernelGGL(mrg_score_keys_kernel, dim3(gr), dim3(256), 0, st, d_scores, d_ids, g, nq, q0, nqc, k,
+                       p2.as<const uint32_t>(), k1.as<uint64_t>());
+    HIPC(hipGetLastError());
+    CHECK(hcr_seg_sort_u64_u32(temp, k1.as<const uint64_t>(), k2.as<uint64_t>(), p2.as<const uint32_t>(),
+                               p1.as<uint32_t>(), items, nqc, offs.as<const int>(), 1, st));
+    hipLaunchKernelGGL(mrg_out_kernel, dim3((unsigned)(((int64_t)nqc * k + 255) / 256)), dim3(256), 0, st,
+                       d_scores, d_ids, g, nq, q0, nqc, k, p1.as<const uint32_t>(), d_out_scores, d_out_ids);
+    HIPC(hipGetLastError());
+  }
+  HIPC(hipStreamSynchronize(st));        // (the scratch buffers are freed on return)
+  return HCR_OK;
+}
+
 extern "C" int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g,
                                      int64_t nq, int k, double* d_out_scores, int64_t* d_out_ids,
                                      void* stream) {
   if (g <= 0 || k <= 0 || nq < 0) return set_err(HCR_EINVAL, "bad merge shape g=%d k=%d", g, k);
-  if ((int64_t)g * k > 8192) return set_err(HCR_EINVAL, "g*k must be <= 8192");
   if (nq == 0) return HCR_OK;
   if (!d_scores || !d_ids || !d_out_scores || !d_out_ids) return set_err(HCR_EINVAL, "NULL buffer");
+  if ((int64_t)g * k > 8192)
+    return merge_sorted(d_scores, d_ids, g, nq, k, d_out_scores, d_out_ids, (hipStream_t)stream);
   const int M = next_pow2(g * k);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(merge_shards_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 16, st,

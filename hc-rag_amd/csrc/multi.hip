@@ -90,7 +90,13 @@ struct hcr_multi_index {
   std::vector<ncclComm_t> comms;
   DevBuf cs, ci, ms, mi;              // on shard 0's device: gathered lists, merged lists
   hcr_search_stats stats{};
+  bool broken = false;                // a failed add could not be rolled back (shard sizes and
+                                      // id maps disagree): every later call refuses
 };
+static int refuse_broken(const hcr_multi_index* m) {
+  return hcr_set_error(HCR_EINTERNAL, "multi-device index unusable: an earlier failed hcr_multi_add "
+                                      "could not be rolled back");
+}
 
 extern "C" int hcr_multi_create(int n_dev, const int* dev_ids, int dim, int dtype,
                                 int64_t capacity_rows, hcr_multi_index** out) {
@@ -154,6 +160,7 @@ extern "C" int hcr_multi_exchange_kind(const hcr_multi_index* m) { return m ? m-
 extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, int rows_dtype,
                              int normalize) {
   if (!m) return hcr_set_error(HCR_EINVAL, "index is NULL");
+  if (m->broken) return refuse_broken(m);
   if (n < 0) return hcr_set_error(HCR_EINVAL, "negative row count");
   if (n == 0) return HCR_OK;
   if (!rows) return hcr_set_error(HCR_EINVAL, "rows is NULL");
@@ -185,10 +192,20 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
     if (rc == HCR_OK && j == fail_shard && m->n > 0) rc = hcr_set_error(HCR_EHIP, "injected failure (HCRAG_FAIL_MULTI_ADD)");
     if (rc != HCR_OK) {
       const std::string msg = hcr_last_error();
+      std::string undo_err;
       for (int i = 0; i <= j; ++i) {
         hcr_multi_shard& t = m->sh[i];
-        if (hcr_index_size(t.ix) > old_rows[i]) (void)hcr_index_truncate_internal(t.ix, old_rows[i]);
-        t.gids.resize(old_gids[i]);
+        if (hcr_index_size(t.ix) > old_rows[i] &&
+            hcr_index_truncate_internal(t.ix, old_rows[i]) != HCR_OK && undo_err.empty())
+          undo_err = hcr_last_error();
+        // (a shard whose truncation failed keeps ids for every row it holds: no search maps a
+        // local row past the end of its id map)
+        t.gids.resize(std::max<size_t>(old_gids[i], (size_t)hcr_index_size(t.ix)));
+      }
+      if (!undo_err.empty()) {
+        m->broken = true;
+        return hcr_set_errorf(HCR_EINTERNAL, "%s; the rollback failed too (%s): the multi-device index "
+                              "is unusable", msg.c_str(), undo_err.c_str());
       }
       return hcr_set_errorf(rc, "%s (hcr_multi_add rolled back: no row of the call was added)", msg.c_str());
     }
@@ -199,6 +216,7 @@ extern "C" int hcr_multi_add(hcr_multi_index* m, const void* rows, int64_t n, in
 
 extern "C" int hcr_multi_set_rowmask(hcr_multi_index* m, const uint8_t* mask, int64_t n) {
   if (!m) return hcr_set_error(HCR_EINVAL, "index is NULL");
+  if (m->broken) return refuse_broken(m);
   if (mask && n != m->n) return hcr_set_errorf(HCR_EINVAL, "mask length %lld != index size %lld",
                                                (long long)n, (long long)m->n);
   std::vector<uint8_t> sub;
@@ -234,8 +252,9 @@ extern "C" int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_
                                 int score_mode, double threshold, double* out_scores,
                                 int64_t* out_ids) {
   if (!m) return hcr_set_error(HCR_EINVAL, "index is NULL");
+  if (m->broken) return refuse_broken(m);
   if (nq < 0) return hcr_set_error(HCR_EINVAL, "negative query count");
-  if (k <= 0 || k > 2048) return hcr_set_errorf(HCR_EINVAL, "k must be in [1, 2048], got %d", k);
+  if (k <= 0) return hcr_set_errorf(HCR_EINVAL, "k must be >= 1, got %d", k);
   if (nq == 0) return HCR_OK;
   if (!queries || !out_scores || !out_ids) return hcr_set_error(HCR_EINVAL, "NULL buffer");
   if (!m->rccl_init) CHECK(init_rccl(m));
@@ -316,7 +335,8 @@ extern "C" int hcr_multi_search(hcr_multi_index* m, const float* queries, int64_
   int lists = g;
   const double* src_s = S;
   const int64_t* src_i = I;
-  const int G = std::max(1, kMergeMaxKeys / k);
+  // (k > kMergeMaxKeys / 2: one call over every list, merged by sorting -- hcr_merge_topk_device)
+  const int G = kMergeMaxKeys / k >= 2 ? kMergeMaxKeys / k : g;
   bool into_m = true;
   CHECK(m->gs.ensure(lst * g * 8));             // cs / ci hold the gathered lists
   CHECK(m->gi.ensure(lst * g * 8));

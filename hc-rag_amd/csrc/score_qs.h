@@ -140,7 +140,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const float* __restrict__ inv_norm, const uint32_t* __restrict__ mask,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles, int tstride,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
-                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp, int prio = 0) {
+                     uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp) {
   using L = QsLayout<NST, KS, RT_, NQ, HS>;
   constexpr int NW = QS_NW;
   using Op = MfmaOp<TM>;
@@ -157,10 +157,6 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // issue priority (A/B hook HCRAG_QS_PRIO): 1 = the second wave of each SIMD (waves 4-7, which
-  // the arbiter otherwise serves last: they finish a tile's MFMAs ~3k cycles after waves 0-3)
-  // raised for the whole kernel
-  if (prio == 1 && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
   const int nwg = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;

@@ -14,26 +14,18 @@ using namespace hcr;
 
 namespace {
 
-int qs_prio() {                 // HCRAG_QS_PRIO (A/B hook, read once): score_qs.h `prio`
-  static const int v = [] {
-    const char* e = getenv("HCRAG_QS_PRIO");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <typename TM, int CAP, int KS, int NQ, int RT, int NST = (RT == 256 ? 4 : 8), int HS = 2>
 void launch_t(const QsArgs& a, hipStream_t st) {
   if (a.unit)
     hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, true, NQ, RT, NST, HS>), dim3(a.nqb * a.P),
                        dim3(QS_NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
                        a.mask, static_cast<const TM*>(a.qhat), a.nqb, a.P, a.ntiles, a.tstride,
-                       a.buf, a.tau_g, a.partials, a.pcnt, a.kp, qs_prio());
+                       a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
   else
     hipLaunchKernelGGL((score_topk_qs_kernel<TM, CAP, KS, false, NQ, RT, NST, HS>), dim3(a.nqb * a.P),
                        dim3(QS_NW * 64), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, a.inv32,
                        a.mask, static_cast<const TM*>(a.qhat), a.nqb, a.P, a.ntiles, a.tstride,
-                       a.buf, a.tau_g, a.partials, a.pcnt, a.kp, qs_prio());
+                       a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP>

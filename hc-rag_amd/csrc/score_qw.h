@@ -32,6 +32,19 @@
 
 namespace hcr {
 
+#ifdef HCR_QW_STAMPS
+// Diagnostic build only (Makefile target `stamps_qw`, tools/qw_stamps.py): per wave of the dense
+// launch, s_memtime cycles summed over the stages: [0] vmcnt wait + barrier, [1] DMA issue +
+// bound reads, [2] the MFMA groups (issue), [3] the epilogue, [4] stages.  Never in the product.
+__device__ unsigned long long hcr_qw_stamps[4096 * 8 * 8];
+#define HCR_QW_STAMP(t)                                                                \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#endif
+
 constexpr int QW_QT = 256;      // queries per workgroup (8 waves x 32; kQwQueries on the host)
 constexpr int QW_NST = 3;       // ring stages
 
@@ -92,21 +105,30 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
 // stages of the sampled 256-row tiles (tile vt * tstride, 256 / SR stages each), partitions are
 // whole 128-row units, and per unit and query the largest coarse score goes to
 // umax[unit][nqb * QT] -- no candidate lists (v4's MAXONLY form is LDS-fill-bound).
-template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false>
+// DM: who issues a stage's LDS-DMA ops and when.  0: every wave its PPW pieces + its bounds,
+// all right after the stage barrier; 1: waves 0-3 only (2 PPW pieces + two waves' bounds each),
+// right after the barrier -- waves 4-7 go straight to their MFMAs; 2: waves 0-3 only, one op
+// per GSTEP MFMA groups over the first 3/4 of them; 3: every wave, spread likewise.
+template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false,
+          int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp,
-                     int tstride = 1, float* __restrict__ umax = nullptr, int old_test = 0) {
+                     int tstride = 1, float* __restrict__ umax = nullptr) {
   using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = L::NST, D = NST - 1;
-  constexpr int OPS = PPW + 1;                       // vmcnt-counted ops per wave per stage
+  // issuing waves, pieces per issuing wave, vmcnt-counted ops per issuing wave per stage
+  constexpr int NIW = (DM == 1 || DM == 2) ? 4 : 8, PPI = L::PIECES / NIW, OPS = PPI + 8 / NIW;
+  constexpr bool SPREAD = DM >= 2;
+  static_assert(L::PIECES % NIW == 0, "pieces per issuing wave");
   // fragment groups per stage: (row-block pair, k-step) for the row-block pairs, then (the odd
   // last row block, k-step pair) when RB is odd
   constexpr int NGP = (RB / 2) * KS, NG = NGP + (RB % 2) * (KS / 2);
+  constexpr int GSTEP = (NG * 3 / 4) / OPS > 0 ? (NG * 3 / 4) / OPS : 1;   // SPREAD: groups per op
   static_assert(CAP >= 128 && CAP % 64 == 0, "candidate buffer");
   __shared__ __attribute__((aligned(16))) char lds[L::TOTAL];
   uint64_t* tau_key = reinterpret_cast<uint64_t*>(lds + L::TAU);
@@ -173,9 +195,10 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                                             0x00020000);
     return d;
   };
+  const bool issuer = NIW == 8 || wave < NIW;
   auto issue_op = [&](const StageDesc& d, int u) __attribute__((always_inline)) {
-    if (u < PPW) {
-      const int j = wave + 8 * u;
+    if (u < PPI) {
+      const int j = wave + NIW * u;
       // the piece's source offset re-derived per stage from an opaque copy of the row pitch:
       // hoisted, the PPW offsets hold PPW SGPRs across the loop (48-row stages: SGPR spills)
       int ldbs = ldb;
@@ -187,16 +210,18 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       int tv;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
                    "v_and_b32 %0, 31, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(tv));
+      const int bw = wave + NIW * (u - PPI);          // the wave whose 32 bounds these are
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * 8 + wave) * 256),
-          4, tv, wq0 * 4, 0, 0);
+          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * 8 + bw) * 256),
+          4, tv, bw * 32 * 4, 0, 0);
     }
   };
-  for (int i = 0; i < D; ++i) {
-    const StageDesc d = stage_desc(i);
+  if (issuer)
+    for (int i = 0; i < D; ++i) {
+      const StageDesc d = stage_desc(i);
 #pragma unroll
-    for (int u = 0; u < OPS; ++u) issue_op(d, u);
-  }
+      for (int u = 0; u < OPS; ++u) issue_op(d, u);
+    }
 
   const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
   const uint32_t lds0 = lds_addr(lds);
@@ -204,17 +229,29 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   bool need = false;
   uint64_t tkr[2] = {0ull, 0ull};
   float umx[2] = {0.f, 0.f};                         // MAXONLY: the current unit's maxima
+#ifdef HCR_QW_STAMPS
+  uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
+#endif
   for (int s = 0; s < nsteps; ++s) {
+#ifdef HCR_QW_STAMPS
+    if constexpr (!MAXONLY) HCR_QW_STAMP(st_t0);
+#endif
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
+#ifdef HCR_QW_STAMPS
+    if constexpr (!MAXONLY) HCR_QW_STAMP(st_t1);
+#endif
     // stage s + D into the slot everyone has finished with, all OPS ops at once: spread over the
     // MFMA groups they cost 10 % fewer wave cycles but the 4 query blocks of a row partition
     // drifted apart and FETCH_SIZE grew 2.6x (their shared L2 reuse broken: DESIGN.md §5)
-    {
-      const StageDesc nd = stage_desc(s + D);
+    if constexpr (!SPREAD) {
+      if (issuer) {
+        const StageDesc nd = stage_desc(s + D);
 #pragma unroll
-      for (int u = 0; u < OPS; ++u) issue_op(nd, u);
+        for (int u = 0; u < OPS; ++u) issue_op(nd, u);
+      }
     }
+    [[maybe_unused]] const StageDesc nd = SPREAD ? stage_desc(s + D) : StageDesc{};
 
     const int slot = s % NST;
     const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
@@ -228,6 +265,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64"
                    : "=&v"(tg2[0]), "=&v"(tg2[1]) : "v"(ta) : "memory");
     }
+#ifdef HCR_QW_STAMPS
+    if constexpr (!MAXONLY) HCR_QW_STAMP(st_t2);
+#endif
     floatx4 acc[RB][2];
 #pragma unroll
     for (int m = 0; m < RB; ++m) acc[m][0] = acc[m][1] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -246,6 +286,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     for (int j = 0; j < FD - 1; ++j) issue(j, av[j]);
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
+      if constexpr (SPREAD) {       // op u at group u * GSTEP (folds to constants when unrolled)
+        if (j % GSTEP == 0 && j / GSTEP < OPS && issuer) issue_op(nd, j / GSTEP);
+      }
       if (j + FD - 1 < NG) {
         issue(j + FD - 1, av[(j + FD - 1) % FD]);
         qw_frag_wait<2 * (FD - 1)>(av[j % FD]);
@@ -272,6 +315,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       }
     }
 
+#ifdef HCR_QW_STAMPS
+    if constexpr (!MAXONLY) HCR_QW_STAMP(st_t3);
+#endif
     // ---- epilogue of tile t0 + s: this wave's 32 queries x SR rows ----
     int le;
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
@@ -314,24 +360,12 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     // ordered key, max(high word of the local k'-th key, global bound) -- no fmaxf sNaN
     // canonicalisation, no key -> float round trips (a NaN maximum passes; its scores fail below)
     bool hit[2];
-    if (old_test) {                // (the r03 test, A/B hook HCRAG_QW_OLDTEST)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const float th = fmaxf(tkr[n] ? key_score(tkr[n]) : -INFINITY, unord32(tg2[n]));
-        float mx = -INFINITY;
+    for (int n = 0; n < 2; ++n) {
+      float mx = qw_max4(acc[0][n]);
 #pragma unroll
-        for (int m = 0; m < RB; ++m)
-          mx = fmaxf(mx, fmaxf(fmaxf(acc[m][n][0], acc[m][n][1]), fmaxf(acc[m][n][2], acc[m][n][3])));
-        hit[n] = mx >= th;
-      }
-    } else {
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        float mx = qw_max4(acc[0][n]);
-#pragma unroll
-        for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
-        hit[n] = qw_ord32(mx) >= max((uint32_t)(tkr[n] >> 32), tg2[n]);
-      }
+      for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
+      hit[n] = qw_ord32(mx) >= max((uint32_t)(tkr[n] >> 32), tg2[n]);
     }
     if (__any(hit[0] || hit[1])) {
       float thr[2];
@@ -377,7 +411,22 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         tkr[1] = v3_lds_u64(tau_key + qle + 16);
       }
     }
+#ifdef HCR_QW_STAMPS
+    if constexpr (!MAXONLY) {
+      HCR_QW_STAMP(st_t4);
+      st_acc[0] += st_t1 - st_t0;
+      st_acc[1] += st_t2 - st_t1;
+      st_acc[2] += st_t3 - st_t2;
+      st_acc[3] += st_t4 - st_t3;
+    }
+#endif
   }
+#ifdef HCR_QW_STAMPS
+  if (!MAXONLY && lane == 0 && b < 4096) {
+    unsigned long long* o = hcr_qw_stamps + ((size_t)b * 8 + wave) * 8;
+    o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = st_acc[3]; o[4] = nsteps;
+  }
+#endif
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (MAXONLY) return;

@@ -14,17 +14,30 @@ using namespace hcr;
 
 namespace {
 
-int old_test() {              // HCRAG_QW_OLDTEST (A/B hook, read once): the r03 stage test
-  static const int v = getenv("HCRAG_QW_OLDTEST") ? 1 : 0;
+int qw_dm() {                 // HCRAG_QW_DM (r05 A/B hook, read once): score_qw.h DM
+  static const int v = [] {
+    const char* e = getenv("HCRAG_QW_DM");
+    return e ? atoi(e) : 0;
+  }();
   return v;
+}
+
+template <typename TM, int CAP, int KS, int SR, int NST, int DM>
+void launch_dense(const QsArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, DM>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
+                     st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
+                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
   if constexpr (256 % SR != 0) {   // (a dense-only stage shape: the pre-pass never asks for it)
-    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                       static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr, old_test());
+    switch (qw_dm()) {
+      case 1: launch_dense<TM, CAP, KS, SR, NST, 1>(a, st); break;
+      case 2: launch_dense<TM, CAP, KS, SR, NST, 2>(a, st); break;
+      case 3: launch_dense<TM, CAP, KS, SR, NST, 3>(a, st); break;
+      default: launch_dense<TM, CAP, KS, SR, NST, 0>(a, st);
+    }
   } else if (a.umax)       // the sampling pre-pass (MAXONLY)
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                        st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
@@ -32,8 +45,7 @@ void launch_t(const QsArgs& a, hipStream_t st) {
   else
     hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
                        static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr,
-                       old_test());
+                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 // Dense-pass stage shape at D = 768: 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows
@@ -84,3 +96,9 @@ int launch_qw(int dtype, const QsArgs& a, hipStream_t st) {
   HIPC(hipGetLastError());
   return HCR_OK;
 }
+
+#ifdef HCR_QW_STAMPS
+extern "C" int hcr_debug_qw_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hcr::hcr_qw_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif

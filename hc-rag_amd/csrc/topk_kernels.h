@@ -641,18 +641,26 @@ __device__ __forceinline__ void acc8_f64(double& acc, const TQ* __restrict__ q, 
 // sorted descending and zero padded, `qd` (LDS) the fp32 query widened to fp64; hi / lo / nrm
 // are kp-slot LDS arrays.  Writes the query's top-k, its certificate flag and s_k.
 template <typename TS>
-__device__ __forceinline__ void rescore_block(const uint64_t* keys, const double* qd, uint64_t* hi,
+__device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, uint64_t* hi,
                                               uint64_t* lo, double* nrm, int* s_nvalid, int q, int kp,
                                               int dim, const double* __restrict__ qnorm,
                                               const double* __restrict__ eps, const TS* __restrict__ rows,
-                                              int ld, const double* __restrict__ norm64, int k, int mode,
+                                              int ld, int64_t n_rows, const double* __restrict__ norm64, int k, int mode,
                                               double thr, int64_t id_offset, double* __restrict__ out_s,
                                               int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
                                               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
                                               uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // Every row this block dereferences (norm64, rows, idmap) comes from a candidate key.  A key
+  // whose row lies outside the index can only come from a defect upstream (a score-kernel or
+  // compaction bug): it is dropped here -- an empty slot -- and flagged in unc_count[1], which
+  // hcr_search turns into HCR_EINTERNAL, instead of faulting the device on the gather.
   for (int c = threadIdx.x; c < kp; c += blockDim.x) {   // row norms gathered up front
-    const uint64_t key = keys[c];
+    uint64_t key = keys[c];
+    if (key && (int64_t)key_row(key) >= n_rows) {
+      keys[c] = key = 0ull;
+      atomicOr(unc_count + 1, 1);
+    }
     nrm[c] = key ? norm64[key_row(key)] : 1.0;
   }
   if (threadIdx.x == 0) *s_nvalid = 0;
@@ -732,13 +740,13 @@ __device__ __forceinline__ void rescore_block(const uint64_t* keys, const double
 
 #define HCR_RESCORE_PARAMS                                                                          \
   const float *__restrict__ q32, int dim, const double *__restrict__ qnorm,                       \
-      const double *__restrict__ eps, const TS *__restrict__ rows, int ld,                          \
+      const double *__restrict__ eps, const TS *__restrict__ rows, int ld, int64_t n_rows,          \
       const double *__restrict__ norm64, int k, int mode, double thr, int64_t id_offset,            \
       double *__restrict__ out_s, int64_t *__restrict__ out_i, int *__restrict__ unc_flags,         \
       int *__restrict__ unc_count, const uint32_t *__restrict__ tau_est,                            \
       uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap
 #define HCR_RESCORE_ARGS                                                                            \
-  q, kp, dim, qnorm, eps, rows, ld, norm64, k, mode, thr, id_offset, out_s, out_i, unc_flags,      \
+  q, kp, dim, qnorm, eps, rows, ld, n_rows, norm64, k, mode, thr, id_offset, out_s, out_i, unc_flags,      \
       unc_count, tau_est, sk_out, idmap
 
 // K4 on a merged list ([q][kp] keys in global memory, merge_lists' last level).
@@ -1152,6 +1160,37 @@ exact_all_kernel(const float* __restrict__ q32, int dim, const double* __restric
     double s = acc / (qnorm[q] * norm64[row]);
     if (mode == 1) s = (s + 1.0) / 2.0;
     out[(int64_t)q * n + row] = s;
+  }
+}
+
+// Deep top-k (k > 2048, hcrag_index.hip deep_topk): every row's exact key for a group of
+// queries -- ord64 of the fp64 cosine in K4's summation order (the same scores bit for bit),
+// 0 for rows outside the row mask -- and its row, to be sorted per query (deep_sort.hip).
+template <typename TS>
+__global__ void __launch_bounds__(256)
+deep_keys_kernel(const float* __restrict__ q32, int dim, const double* __restrict__ qnorm,
+                 const TS* __restrict__ rows, int ld, int64_t n, const double* __restrict__ norm64,
+                 const uint32_t* __restrict__ maskbits, uint64_t* __restrict__ keys,
+                 uint32_t* __restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = blockIdx.y;
+  if (row >= n) return;
+  const bool live = !maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u);
+  double acc = 0.0;
+  if (live) {
+    const float* qs = q32 + (int64_t)q * dim;
+    const TS* e = rows + row * ld;
+    for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+      float x[8];
+      load8_f32(e + d0, x);
+      acc8_f64(acc, qs, d0, dim, x);
+    }
+    acc = wave_sum_f64(acc);
+  }
+  if (lane == 0) {
+    keys[(int64_t)q * n + row] = live ? ord64(acc / (qnorm[q] * norm64[row])) : 0ull;
+    vals[(int64_t)q * n + row] = (uint32_t)row;
   }
 }
 

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "HCRAG_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libhcrag_hip.so"))
 
-HCR_OK, HCR_EINVAL, HCR_EHIP, HCR_ERCCL, HCR_ENOMEM, HCR_EIO = 0, -1, -2, -3, -4, -5
+HCR_OK, HCR_EINVAL, HCR_EHIP, HCR_ERCCL, HCR_ENOMEM, HCR_EIO, HCR_EINTERNAL = 0, -1, -2, -3, -4, -5, -6
 HCR_F16, HCR_BF16, HCR_F32 = 0, 1, 2
 HCR_SCORE_COSINE, HCR_SCORE_UNIT = 0, 1
 

@@ -141,7 +141,7 @@ class VectorIndex:
     # -- queries ------------------------------------------------------------------------
     def search(self, queries, k: int, score_mode: int = HCR_SCORE_COSINE,
                threshold: float = -np.inf):
-        """Exact top-k per query (1 <= k <= 2048).  Returns (scores float64 [nq,k] -- the exact
+        """Exact top-k per query (any k >= 1; above 2048 by a sorted full scan).  Returns (scores float64 [nq,k] -- the exact
         fp64 cosine, mapped by ``score_mode`` --, ids int64 [nq,k]); -1 = empty slot."""
         q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))
         if q.shape[1] != self.dim:

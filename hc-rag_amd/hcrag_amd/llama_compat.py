@@ -24,8 +24,8 @@ Semantics kept from the reference path (``SimpleVectorStore.query`` -> ``get_top
 cosine similarity in fp64, best ``similarity_top_k`` first, ids are the node ids, ``filters``
 (ExactMatch / EQ on metadata keys) restrict the candidate rows.  Differences on purpose: exact
 ties are ordered by insertion order (llama-index's heap order keeps the later node on a tie);
-zero-norm rows score 0 (llama-index yields NaN); similarity_top_k above 2048 raises instead of
-scanning in Python.
+zero-norm rows score 0 (llama-index yields NaN).  Any similarity_top_k >= 1 is served (above
+2048 by the library's sorted full scan, hcrag_index.hip deep_topk).
 """
 from __future__ import annotations
 
@@ -42,7 +42,7 @@ from .index import VectorIndex
 
 _log = logging.getLogger(__name__)
 
-MAX_TOP_K = 2048          # hcr_search's limit (exact for every k up to it)
+MAX_TOP_K = None          # hcr_search takes any k >= 1 (r05: k > 2048 by the sorted full scan)
 
 try:  # pragma: no cover - llama_index is absent in this image
     from llama_index.core.vector_stores.types import (BasePydanticVectorStore,  # type: ignore
@@ -194,8 +194,8 @@ def _filter_pairs(filters) -> List[tuple]:
 
 def _check_top_k(k: int) -> int:
     k = int(k or 1)
-    if k < 1 or k > MAX_TOP_K:
-        raise ValueError(f"similarity_top_k must be in [1, {MAX_TOP_K}], got {k}")
+    if k < 1:
+        raise ValueError(f"similarity_top_k must be >= 1, got {k}")
     return k
 
 

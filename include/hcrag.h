@@ -32,7 +32,9 @@ typedef enum {
   HCR_EHIP = -2,     /* HIP runtime error */
   HCR_ERCCL = -3,    /* RCCL error (multi-device index exchange) */
   HCR_ENOMEM = -4,   /* device allocation failed */
-  HCR_EIO = -5       /* file / format error (encoder weights, vocab) */
+  HCR_EIO = -5,      /* file / format error (encoder weights, vocab) */
+  HCR_EINTERNAL = -6 /* internal consistency check failed (e.g. a candidate key naming a row
+                        outside the index): the call is abandoned, the handle stays usable */
 } hcr_status;
 
 typedef enum { HCR_F16 = 0, HCR_BF16 = 1, HCR_F32 = 2 } hcr_dtype;
@@ -108,7 +110,8 @@ int hcr_index_set_rowmask(hcr_index* index, const uint8_t* mask, int64_t n);
  * queries the certificate cannot settle and for k > 256, an exact fp64 scan of every row.
  * Replaces cosine_similarity + np.argsort(...)[::-1][:top_k] + threshold filter of
  * experiments/main.py:841-849 (and :886-889), and get_top_k_embeddings behind
- * VectorContextRetriever (query_interface.py:200-204).  1 <= k <= 2048. */
+ * VectorContextRetriever (query_interface.py:200-204).  Any k >= 1: above 2048 every row's
+ * exact key is sorted per query (query groups of <= 4 GiB of keys; corpora of < 2^31 rows). */
 int hcr_search(hcr_index* index, const float* queries, int64_t nq, int k, int score_mode,
                double threshold, double* out_scores, int64_t* out_ids);
 
@@ -171,7 +174,8 @@ int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)
  * into the global top-k (score desc, id asc).  Used after the cross-GPU exchange of
- * SURVEY.md §8(e).  Asynchronous on `stream`. */
+ * SURVEY.md §8(e).  Asynchronous on `stream` for g x k <= 8192; deeper merges (two stable
+ * segmented sorts per query) synchronise `stream` before returning. */
 int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, int64_t nq,
                           int k, double* d_out_scores, int64_t* d_out_ids, void* stream);
 
@@ -244,7 +248,11 @@ typedef struct hcr_encoder hcr_encoder;
  *   HCR_F32  reference precision (the reference encodes in fp32 torch,
  *            experiments/embedding_generator.py:124): projection GEMMs as three-term split-f16
  *            MFMA products (~22-bit operands, fp32 accumulation), fp32 attention/softmax/
- *            LayerNorm/residual; matches fp32 BertModel to ~1e-6;
+ *            LayerNorm/residual; matches fp32 BertModel to ~1e-6.  The last partly filled
+ *            round of a projection runs as K-chunks summed in chunk order, and which tiles
+ *            fall in that round depends on the batch's packed token count: a sequence's bits
+ *            are deterministic for a given batch but may differ by fp32 rounding (<= 1e-5)
+ *            between batches that contain it (torch's own GEMMs are batch-dependent likewise);
  *   HCR_F16 / HCR_BF16  fast: f16 / bf16 MFMA operands (accumulation, LayerNorm, softmax and
  *            the residual stream fp32). */
 int hcr_encoder_create(int device, const hcr_bert_config* cfg, int compute_dtype,

@@ -447,8 +447,41 @@ def test_two_stream_split_bit_identical(tmp_path, dtype, monkeypatch):
     _check(got, _ref_embed(m, ids, mask, "cls"), dtype)
 
 
+def _split_plan(N, K, T, ncu=256, can192=True):
+    """encoder.hip split_plan restated: (feature width, whole tiles, remainder tiles, chunks)."""
+    ntt = (T + 255) // 256
+    best, best_us = None, 1e30
+    for ft in (192, 256):
+        if ft == 192 and not can192:
+            continue
+        nt = -(-N // ft) * ntt
+        full, rem = nt // ncu * ncu, nt % ncu
+        ns = min(ncu // rem, K // 32, 8) if rem else 0
+        w = 0.86 if ft == 192 else 1.0
+        if ns < 2:
+            full, rem, ns = nt, 0, 0
+            us = -(-nt // ncu) * w * 60.0 * K / 768
+        else:
+            us = (full // ncu + 1.0 / ns) * w * 60.0 * K / 768 + 9.0 + 4.3 * ns
+        if us < best_us:
+            best, best_us = (ft, full, rem, ns), us
+    return best
+
+
+def _chunks_straddle_xcds(rem, ns):
+    """gemm_split_kernel's XCD-aware remap (g = contiguous ranges per XCD, block b on XCD b % 8
+    under round-robin dispatch): does some tile's chunk set span two XCDs (two L2s)?"""
+    nwg = rem * ns
+    q8, r8 = nwg >> 3, nwg & 7
+    xcd = {}
+    for b in range(nwg):
+        x = b & 7
+        xcd[(x * (q8 + 1) if x < r8 else r8 * (q8 + 1) + (x - r8) * q8) + (b >> 3)] = x
+    return any(len({xcd[t * ns + c] for c in range(ns)}) > 1 for t in range(rem))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1100, 60])
+@pytest.mark.parametrize("n", [1100, 1000, 60])
 def test_split_gemm_last_round(tmp_path, n):
     """The reference-precision GEMM's K-split of a partly filled last round (encoder.hip
     split_plan / launch_gemm_split, gemm_v4.h gemm_split_kernel<SPLIT> / split_gather): at T ~
@@ -457,7 +490,10 @@ def test_split_gemm_last_round(tmp_path, n):
     tiles than compute units and runs split only.  The chunks are summed in chunk order by
     whichever arrives last, so two runs are the same bits; the split moves the fp32 sums by
     rounding only: within 1e-5 of whole-tile rounds (HCRAG_SPLIT_NONE=1, child process: the
-    hook is read once per process) and within the f32 bar of fp32 BertModel."""
+    hook is read once per process) and within the f32 bar of fp32 BertModel.  n = 1000 (ADVICE
+    r4): every projection's remainder tiles have chunks on two XCDs -- the cross-L2 hand-off of
+    split_gather (sc1 write-through slabs, drained, an agent-scope ticket, sc1 loads) that the
+    bench's 97-token-tile batches run."""
     import json
     import os
     import subprocess
@@ -468,10 +504,18 @@ def test_split_gemm_last_round(tmp_path, n):
     rng = np.random.default_rng(31)
     S = 32
     ids, mask = _batch(rng, n, S, cfg["vocab_size"], lens=rng.integers(16, S + 1, size=n))
+    if n == 1000:
+        T = int(np.asarray(mask).sum())
+        H, I = cfg["hidden_size"], cfg["intermediate_size"]
+        plans = [_split_plan(H, H, T), _split_plan(3 * H, H, T), _split_plan(I, H, T, can192=False),
+                 _split_plan(H, I, T)]
+        assert all(p[3] >= 2 and _chunks_straddle_xcds(p[2], p[3]) for p in plans), (T, plans)
     enc = _encoder(conf, m, "f32", pooling="cls")
     a = enc.encode_ids(ids, mask)
     b = enc.encode_ids(ids, mask)
     np.testing.assert_array_equal(a, b)
+    for _ in range(3):                       # repeated runs: the same bits every time
+        np.testing.assert_array_equal(enc.encode_ids(ids, mask), a)
     inp = str(tmp_path / "in.npz")
     np.savez(inp, ids=ids, mask=mask, dtype="f32", cfg=json.dumps(config_from_hf(conf.to_dict(), "cls", True)),
              **{"sd_" + k: v.numpy() for k, v in m.state_dict().items()})

@@ -90,8 +90,15 @@ def test_vector_store_large_top_k_and_replace():
     res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=2))
     assert res.ids[0] == "n5" and abs(res.similarities[0] - 1.0) < 1e-6
     assert "n5" not in res.ids[1:]
+    # similarity_top_k past the corpus (and past 2048: the sorted full scan) -> every row, ranked
+    E2 = E.copy()
+    E2[5] = q
+    res = vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=5000))
+    es, ei = O.cosine_topk(q[None].astype(np.float32), E2.astype(np.float32), 3000)
+    assert res.ids == [f"n{i}" for i in ei[0]]
+    np.testing.assert_allclose(res.similarities, es[0], rtol=0, atol=1e-6)
     with pytest.raises(ValueError):
-        vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=5000))
+        vs.query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=-1))
 
 
 def test_vector_store_deletes_compact_hbm():

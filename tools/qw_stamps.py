@@ -1,0 +1,50 @@
+"""Where the QW score kernel's dense launch spends a stage, from the stamps build (Makefile target
+`stamps_qw`):
+
+    HCRAG_LIB=hc-rag_amd/lib/stamps_qw/libhcrag_hip.so python tools/qw_stamps.py ROWS DIM BATCH
+
+Runs a few searches on a synthetic L2-normalised corpus, then reads the per-wave s_memtime sums
+of the last dense QW launch: stage wait (vmcnt + barrier), DMA issue + bound reads, MFMA groups
+(issue), epilogue; prints cycles per stage for all waves and for each half of the workgroup
+(waves 0-3 / 4-7: the two waves of each SIMD).  The stamps' own lgkmcnt waits change the timing:
+read shares, not absolute lengths."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hc-rag_amd")]
+import bench  # noqa: E402
+import hcrag_amd  # noqa: E402
+from hcrag_amd import _lib  # noqa: E402
+
+N, D, B = (int(x) for x in sys.argv[1:4])
+dev = torch.device("cuda:0")
+ix = hcrag_amd.VectorIndex(D, "f16", device=0, capacity=N)
+bench.make_shard(ix, hcrag_amd, 0, N, D, "f16", dev)
+Q = np.random.default_rng(1).standard_normal((B, D)).astype(np.float32)
+for _ in range(3):
+    ix.search(Q, 32)
+st = ix.last_stats()
+fn = _lib.lib().hcr_debug_qw_stamps
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+n = 4096 * 8 * 8
+buf = (ctypes.c_ulonglong * n)()
+assert fn(buf, n) == 0
+a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8, 8).astype(np.float64)
+parts = ["wait+barrier", "dma+bounds", "mfma groups", "epilogue"]
+print(f"score_kernel {st['score_kernel']} workgroups {st['workgroups']}")
+for name, sel in (("all waves", slice(0, 8)), ("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
+    sub = a[:, sel, :]
+    live = sub[:, :, 4] > 0
+    stages = sub[:, :, 4][live]
+    tot = sum(sub[:, :, i][live].sum() for i in range(4))
+    print(f"{name}: {live.sum()} waves, {stages.mean():.0f} stages per wave, "
+          f"{tot / stages.sum():.0f} cycles per stage")
+    for i, nm in enumerate(parts):
+        x = sub[:, :, i][live] / stages
+        print(f"  {nm:14s} {x.mean():8.0f} cycles/stage (p10 {np.percentile(x, 10):7.0f}, "
+              f"p90 {np.percentile(x, 90):7.0f})  share {sub[:, :, i][live].sum() / tot:.3f}")
