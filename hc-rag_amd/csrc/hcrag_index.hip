@@ -57,15 +57,17 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
+      w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt, w_psync;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
-      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp;
+      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
   int opt_qs = 0;               // HCR_OPT_QS_FORM (0: the heuristic)
   int opt_prepass = 0;          // HCR_OPT_PREPASS (0: the heuristic)
+  int opt_qw_dm = -1;           // HCR_OPT_QW_DM (-1: the default)
+  int opt_qw_min = 0;           // HCR_OPT_QW_MIN (0: the heuristic)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -135,10 +137,10 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
                    &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax, &ix->w_sk,
-                   &ix->w_pcnt, &ix->w_mcnt,
+                   &ix->w_pcnt, &ix->w_mcnt, &ix->w_psync,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
-                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp};
+                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est};
   for (DevBuf* b : all) b->release();
   if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
@@ -434,6 +436,14 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       if (value < 0 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_PREPASS value %d not in [0, 2]", value);
       ix->opt_prepass = value;
       return HCR_OK;
+    case HCR_OPT_QW_DM:
+      if (value < -1 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_QW_DM value %d not in [-1, 4]", value);
+      ix->opt_qw_dm = value;
+      return HCR_OK;
+    case HCR_OPT_QW_MIN:
+      if (value < 0) return set_err(HCR_EINVAL, "HCR_OPT_QW_MIN value %d negative", value);
+      ix->opt_qw_min = value;
+      return HCR_OK;
     case HCR_OPT_QS_FORM:
       if (value != 0 && value != 1 && value != 3)
         return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not 0, 1 or 3", value);
@@ -552,14 +562,15 @@ struct V3Cfg { int rt, qt, nst; bool qs, qw = false, qw1 = false; int hs = 2; };
 // qw_ok / qw1_ok: a UNIT-capable corpus without a row mask and k' small enough for the
 // QW / QW1 candidate buffers; opt_qw1: HCR_OPT_QW1; opt_qs: HCR_OPT_QS_FORM
 static V3Cfg v3_cfg(int nq, int64_t n_rows, int ld, bool unit_ok, bool qw_ok, bool qw1_ok, int opt_qw1,
-                    int opt_qs = 0) {
+                    int opt_qs = 0, int opt_qw_min = 0) {
   if (nq <= 16) return {256, 16, 8, false};
   // > 256 queries (MFMA-bound): 256 queries per workgroup held in VGPRs, only rows streamed
   // through LDS -- half of v4's LDS-DMA fill per flop (score_qw.h)
   // From 129 queries at D = 768 (r02 sweeps at 10M x 768: B = 160 3.64 vs 4.48 ms on QS,
-  // B = 256 3.73 vs 4.61); at D = 384 QS and QW tie at 129-256 (1M x 384, B = 256: 0.283 vs
-  // 0.282 ms), so QW from 257 there.
-  const int qw_from = hooks().qw_min > 0 ? hooks().qw_min : (ld / V3_BK >= 24 ? 129 : 257);
+  // B = 256 3.73 vs 4.61) and at D = 384 (r05c, 1M x 384, B = 256 -- configs[1] --, interleaved
+  // in one process: QW with its stage DMA spread over the MFMA groups 0.323 ms per search, QS
+  // 0.330; QW with DMA at the barrier 0.335).
+  const int qw_from = opt_qw_min > 0 ? opt_qw_min : hooks().qw_min > 0 ? hooks().qw_min : 129;
   // QW1: 48 queries per wave at one wave per SIMD, D = 1024 only.  D = 1024 has no other
   // query-stationary kernel (256 queries x 1024 do not fit QW's waves), so it takes QW1 from 257
   // queries unless HCR_OPT_QW1 = 0 (v4 then).
@@ -670,6 +681,9 @@ static int launch_qw_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
   QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
            a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
+  CHECK(ix->w_psync.ensure((size_t)std::max(a.P, 1) * 4));
+  q.psync = ix->w_psync.as<uint32_t>();
+  q.dm = ix->opt_qw_dm;
   return launch_qw(ix->dtype, q, st);
 }
 
@@ -959,7 +973,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const bool qwable = !ix->has_mask && ix->dtype != HCR_F32;
   const V3Cfg c3 = v3_cfg(nq, ix->n, ix->ld, ix->unit_dev_host <= kUnitDevMax,
                           qwable && qw_cap(kp, ix->ld, (nq + kQwQueries - 1) / kQwQueries) > 0, qwable && qw1_cap(kp, ix->ld) > 0,
-                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qs);
+                          ix->opt_qw1 >= 0 ? ix->opt_qw1 : hooks().qw1, ix->opt_qs, ix->opt_qw_min);
   const int ver = (ix->dtype == HCR_F32 || !v3_fits(ix, c3)) ? 1 : 3;
   if (hooks().debug_cfg)
     fprintf(stderr, "[hcrag] search_pass nq=%d n=%lld ld=%d kp=%d unit_dev=%.3g rho=%.3g mask=%d "
@@ -1070,10 +1084,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
         CHECK(ix->w_umax.ensure((size_t)U * nqpad * 4));
         // the sampled tiles on QW when the dense pass is QW (its MAXONLY form, score_qw.h; r03:
         // v4's form is LDS-fill-bound), on v4 otherwise; HCR_OPT_PREPASS 1 / 2 force v4 / QW
-        if (qw && ix->opt_prepass != 1) {
+        // (under QS: QW's form when HCR_OPT_PREPASS = 2 on a UNIT corpus without a row mask)
+        const bool qw_pre = qw ? ix->opt_prepass != 1
+                               : (qs && ix->opt_prepass == 2 && unit && !ix->has_mask && qw_supported(ix->ld));
+        if (qw_pre) {
           QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, nqb_pre,
                    a.P, a.nvt * (256 / qw_sample_rows(ix->ld)), a.tstride, ix->w_buf.as<uint64_t>(),
-                   ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), kp, cap,
+                   ix->w_taug.as<uint32_t>(), ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), kp, 256,
                    true, 0};
           q.umax = ix->w_umax.as<float>();
           CHECK(launch_qw(ix->dtype, q, st));
@@ -1197,9 +1214,12 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   const bool mf = ix->dtype != HCR_F32 && (ksteps == 12 || ksteps == 24 || ksteps == 32) &&
                   !hooks().no_mfma_filter;
   if (mf) CHECK(refresh_norm_stats(ix));
-  const unsigned mgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32, 2048));
+  // MFMA-prefiltered scans take up to kFbGroupsPerScan query groups at once (one pass over the
+  // rows for all of them); the fp64 scan (K6) one group
+  const int super = mf ? kFallbackGroup * kFbGroupsPerScan : kFallbackGroup;
+  const int64_t mchunks = round_up(std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32, 2048)), 8);
 #define MFIL(TS, KS, HIST)                                                                        \
-  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, HIST>), dim3(mgrid), dim3(256), 0, st,     \
+  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, HIST>), dim3((unsigned)(mchunks * ngr)), dim3(256), 0, st, \
                      ix->f_qhat.as<const TS>(), ix->f_eps.as<const double>(), ix->f_q.as<const float>(), \
                      ng, ix->dim, ix->f_qn.as<const double>(), ix->rows.as<const TS>(), ix->ld, ix->n, \
                      ix->inv32.as<const float>(), ix->norm64.as<const double>(),                 \
@@ -1209,23 +1229,26 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>(),        \
-                     ix->f_ch.as<unsigned int>())
+                     ix->f_ch.as<unsigned int>(), ngr, hstride)
 #define MFIL_KS(TS, HIST)                                                                         \
   do {                                                                                            \
     if (ksteps == 12) MFIL(TS, 12, HIST); else if (ksteps == 24) MFIL(TS, 24, HIST); else MFIL(TS, 32, HIST); \
   } while (0)
-  auto launch_mfil = [&](int ng, bool hist) {
+  auto launch_mfil = [&](int ng, bool hist, int hstride) {
+    const int ngr = (ng + kFallbackGroup - 1) / kFallbackGroup;
     if (ix->dtype == HCR_F16) { if (hist) MFIL_KS(_Float16, true); else MFIL_KS(_Float16, false); }
     else { if (hist) MFIL_KS(__bf16, true); else MFIL_KS(__bf16, false); }
   };
-  for (size_t g0 = 0; g0 < idx.size(); g0 += kFallbackGroup) {
-    const int ng = (int)std::min<size_t>(kFallbackGroup, idx.size() - g0);
+  for (size_t g0 = 0; g0 < idx.size(); g0 += super) {
+    const int ng = (int)std::min<size_t>(super, idx.size() - g0);
+    const int ngpad = (int)round_up(ng, kFallbackGroup);
     CHECK(ix->f_idx.ensure((size_t)ng * 4));
     CHECK(ix->f_q.ensure((size_t)ng * ix->dim * 4));
     CHECK(ix->f_qn.ensure((size_t)ng * 8));
     CHECK(ix->f_thh.ensure((size_t)ng * 8));
     CHECK(ix->f_thl.ensure((size_t)ng * 8));
     CHECK(ix->f_act.ensure((size_t)ng * 4));
+    CHECK(ix->f_est.ensure((size_t)ng * 4));
     CHECK(ix->f_cnt.ensure((size_t)ng * 4));
     CHECK(ix->f_bufh.ensure((size_t)ng * cap * 8));
     CHECK(ix->f_bufl.ensure((size_t)ng * cap * 8));
@@ -1235,7 +1258,7 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     CHECK(ix->f_hcnt.ensure((size_t)ng * (kFbBins + 1) * 4));
     CHECK(ix->f_hmin.ensure((size_t)ng * (kFbBins + 1) * 8));
     std::vector<uint64_t> thh(sk.begin() + g0, sk.begin() + g0 + ng), thl(ng, 0ull);
-    std::vector<int> act(ng, 1);
+    std::vector<int> act(ng, 1), est(ng, 0);
     // histogram range of the first round: [score of the starting threshold, just above 1]
     std::vector<double> hlo(ng), hhi(ng, 1.0 + 1e-6);
     for (int i = 0; i < ng; ++i) {
@@ -1252,24 +1275,26 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(ix->f_thl.p, thl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(ix->f_act.p, act.data(), (size_t)ng * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemsetAsync(ix->f_est.p, 0, (size_t)ng * 4, st));
     hipLaunchKernelGGL(gather_rows_f32, dim3(ng), dim3(256), 0, st, qc, ix->f_idx.as<const int>(), ng,
                        ix->dim, ix->f_q.as<float>());
     hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
                        ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
     HIPC(hipGetLastError());
     if (mf) {
-      // the group's unit MFMA-dtype queries and eps_q for the non-UNIT coarse score c =
-      // fl(q^.e . inv32); padded to kFallbackGroup with zero queries
-      CHECK(ix->f_qhat.ensure((size_t)kFallbackGroup * ix->ld * 2));
-      CHECK(ix->f_eps.ensure((size_t)kFallbackGroup * 8));
-      CHECK(ix->f_tmp.ensure(1024));
+      // the groups' unit MFMA-dtype queries and eps_q for the non-UNIT coarse score c =
+      // fl(q^.e . inv32); padded to whole groups with zero queries
+      CHECK(ix->f_qhat.ensure((size_t)ngpad * ix->ld * 2));
+      CHECK(ix->f_eps.ensure((size_t)ngpad * 8));
+      CHECK(ix->f_tmp.ensure((size_t)ngpad * 24 + 64));
       char* tmp = ix->f_tmp.as<char>();
 #define PREP(TM)                                                                                   \
-  hipLaunchKernelGGL((prep_queries_kernel<TM>), dim3((kFallbackGroup + 3) / 4), dim3(256), 0, st,     \
-                     ix->f_q.as<const float>(), ng, kFallbackGroup, ix->dim, ix->ld, ix->f_qhat.as<TM>(), \
+  hipLaunchKernelGGL((prep_queries_kernel<TM>), dim3((ngpad + 3) / 4), dim3(256), 0, st,           \
+                     ix->f_q.as<const float>(), ng, ngpad, ix->dim, ix->ld, ix->f_qhat.as<TM>(),    \
                      reinterpret_cast<double*>(tmp), ix->f_eps.as<double>(), ix->rho_host,            \
-                     accum_gamma(ix->ld), -1.0, reinterpret_cast<uint32_t*>(tmp + 256),              \
-                     reinterpret_cast<uint32_t*>(tmp + 384), reinterpret_cast<int*>(tmp + 512))
+                     accum_gamma(ix->ld), -1.0, reinterpret_cast<uint32_t*>(tmp + (size_t)ngpad * 8), \
+                     reinterpret_cast<uint32_t*>(tmp + (size_t)ngpad * 12),                          \
+                     reinterpret_cast<int*>(tmp + (size_t)ngpad * 16))
       if (ix->dtype == HCR_F16) PREP(_Float16); else PREP(__bf16);
 #undef PREP
       HIPC(hipGetLastError());
@@ -1277,9 +1302,19 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
       for (int i = 0; i < ng; ++i) need0 |= thh[i] == 0ull;
       if (need0) {
         // round 0 (K6h): coarse histograms -> a starting threshold T_q <= the true k-th best
-        CHECK(ix->f_ch.ensure((size_t)kFallbackGroup * kFbHistBins * 4));
+        CHECK(ix->f_ch.ensure((size_t)ngpad * kFbHistBins * 4));
         HIPC(hipMemsetAsync(ix->f_ch.p, 0, (size_t)ng * kFbHistBins * 4, st));
-        launch_mfil(ng, true);
+        // on a corpus of >= 100 k rows per sampled stride (10M rows, k <= 6250: 16), a sample
+        // of runs of 4 16-row tiles, one in hstride: an estimated threshold (see K6h)
+        int hstride = 1;
+        while (hstride < 16 && ix->n / (2 * hstride) >= (int64_t)100 * k) hstride *= 2;
+        const int64_t ntile16 = (ix->n + 15) / 16, run = 4 * (int64_t)hstride;
+        const int64_t stiles = ntile16 / run * 4 + std::min<int64_t>(4, ntile16 % run);
+        const double frac = std::min(1.0, (double)(stiles * 16) / (double)ix->n);
+        const double fk = frac * k;
+        const uint64_t need_rows = hstride == 1 ? (uint64_t)k
+                                                : (uint64_t)std::ceil(fk + 5.0 * std::sqrt(fk) + 3.0);
+        launch_mfil(ng, true, hstride);
         HIPC(hipGetLastError());
         std::vector<unsigned int> hist((size_t)ng * kFbHistBins);
         std::vector<double> epsq(ng);
@@ -1292,7 +1327,8 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
           uint64_t acc = 0;
           for (int b = kFbHistBins - 1; b >= 0; --b) {
             acc += hist[(size_t)i * kFbHistBins + b];
-            if (acc >= (uint64_t)k) {
+            if (acc >= need_rows) {
+              est[i] = hstride > 1 ? 1 : 0;
               // >= k rows have c >= edge (less the float binning's rounding), so exact >= T
               const double T = (-kFbHistRange + b * bw) - 1e-5 - epsq[i];
               uint64_t u;
@@ -1305,6 +1341,8 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
         }
         HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
         HIPC(hipMemcpyAsync(ix->f_hlo.p, hlo.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(ix->f_est.p, est.data(), (size_t)ng * 4, hipMemcpyHostToDevice, st));
+        HIPC(hipStreamSynchronize(st));     // (the host vectors above are copied from)
         ix->stats.fallback_rounds += 1;
       }
     }
@@ -1328,7 +1366,7 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>())
-      if (mf) launch_mfil(ng, false);
+      if (mf) launch_mfil(ng, false, 1);
       else if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
 #undef FIL
       hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
@@ -1338,7 +1376,7 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                          thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
                          ix->f_idx.as<const int>(), os, oi, ix->f_hlo.as<double>(),
                          ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
-                         ix->f_hmin.as<const unsigned long long>());
+                         ix->f_hmin.as<const unsigned long long>(), ix->f_est.as<int>());
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&again, ix->f_again.p, 4, hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));

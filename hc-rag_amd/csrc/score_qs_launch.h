@@ -23,6 +23,8 @@ struct QsArgs {
                              // KS = 12)
   float* umax = nullptr;     // QW: the MAXONLY sampling pre-pass into umax[unit][nqb * 256]
                              // (ntiles = virtual stages of the sampled tiles, tstride their stride)
+  uint32_t* psync = nullptr; // QW dense pass: one arrival counter per row partition (P words)
+  int dm = -1;               // QW dense pass: DMA-issue mode (score_qw.h DM; -1 = the default)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128

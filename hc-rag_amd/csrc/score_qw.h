@@ -47,6 +47,8 @@ __device__ unsigned long long hcr_qw_stamps[4096 * 8 * 8];
 
 constexpr int QW_QT = 256;      // queries per workgroup (8 waves x 32; kQwQueries on the host)
 constexpr int QW_NST = 3;       // ring stages
+constexpr int QW_PS_EVERY = 2;  // DM 4: stages per partition sync point
+constexpr int QW_PS_LAG = 1;    // ... sync points a workgroup may run ahead of its slowest sibling
 
 // rows per stage for KS 32-deep k-steps: 48 KiB stages (RB = SR / 16 row blocks, even)
 constexpr int qw_sr(int ks) { return ks == 24 ? 32 : ks == 12 ? 64 : 0; }
@@ -108,7 +110,11 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
 // DM: who issues a stage's LDS-DMA ops and when.  0: every wave its PPW pieces + its bounds,
 // all right after the stage barrier; 1: waves 0-3 only (2 PPW pieces + two waves' bounds each),
 // right after the barrier -- waves 4-7 go straight to their MFMAs; 2: waves 0-3 only, one op
-// per GSTEP MFMA groups over the first 3/4 of them; 3: every wave, spread likewise.
+// per GSTEP MFMA groups over the first 3/4 of them; 3: every wave, spread likewise; 4: as 3, and
+// the nqb workgroups of a row partition (the query blocks that share each row stage through
+// their XCD's L2) kept within QW_PS_LAG sync points of each other by an arrival counter per
+// partition (psync[p], zeroed per launch): spread issue alone lets them drift apart and the row
+// stages are fetched from HBM once per query block instead of once (r05b: FETCH_SIZE 2.65x).
 template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false,
           int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
@@ -116,14 +122,15 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp,
-                     int tstride = 1, float* __restrict__ umax = nullptr) {
+                     int tstride = 1, float* __restrict__ umax = nullptr,
+                     uint32_t* __restrict__ psync = nullptr) {
   using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = L::NST, D = NST - 1;
   // issuing waves, pieces per issuing wave, vmcnt-counted ops per issuing wave per stage
   constexpr int NIW = (DM == 1 || DM == 2) ? 4 : 8, PPI = L::PIECES / NIW, OPS = PPI + 8 / NIW;
-  constexpr bool SPREAD = DM >= 2;
+  constexpr bool SPREAD = DM >= 2, PSYNC = DM == 4 && !MAXONLY;
   static_assert(L::PIECES % NIW == 0, "pieces per issuing wave");
   // fragment groups per stage: (row-block pair, k-step) for the row-block pairs, then (the odd
   // last row block, k-step pair) when RB is odd
@@ -232,12 +239,46 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #ifdef HCR_QW_STAMPS
   uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
 #endif
+  // DM 4: the partition's arrival count, loaded one stage ahead of its check (wave 0)
+  const bool psync_on = PSYNC && psync != nullptr && nqb > 1 && wave == 0;
+  uint32_t ps_seen = 0;
+  int ps_budget = 1 << 14;           // total spins before this workgroup stops waiting (a sibling
+                                     // not resident -- never the case at one workgroup per CU)
   for (int s = 0; s < nsteps; ++s) {
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t0);
 #endif
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
+    if constexpr (PSYNC) {
+      if (psync_on && s % QW_PS_EVERY == 0 && s / QW_PS_EVERY > QW_PS_LAG) {
+        const uint32_t target = (uint32_t)nqb * (uint32_t)(s / QW_PS_EVERY - QW_PS_LAG);
+        if (__builtin_amdgcn_readfirstlane(ps_seen) < target && ps_budget > 0) {
+          // the bounded spin as one asm block (a compiler-visible loop here spilled the query
+          // fragments): sc1 loads of the counter, s_sleep between them
+          uint32_t v;
+          asm volatile(
+              "1:\n\t"
+              "s_sleep 2\n\t"
+              "global_load_dword %[v], %[a], off sc1\n\t"
+              "s_waitcnt vmcnt(0)\n\t"
+              "v_readfirstlane_b32 %[t], %[v]\n\t"
+              "s_sub_u32 %[b], %[b], 1\n\t"
+              "s_cmp_ge_u32 %[t], %[g]\n\t"
+              "s_cbranch_scc1 2f\n\t"
+              "s_cmp_gt_i32 %[b], 0\n\t"
+              "s_cbranch_scc1 1b\n"
+              "2:"
+              : [v] "=&v"(v), [t] "=&s"(ps_seen), [b] "+s"(ps_budget)
+              : [a] "v"(psync + p), [g] "s"(target)
+              : "memory", "scc");
+        }
+      }
+    }
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
+    if constexpr (PSYNC) {
+      if (psync_on && s % QW_PS_EVERY == 0 && __builtin_amdgcn_mbcnt_lo(~0u, 0) == 0)
+        __hip_atomic_fetch_add(psync + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t1);
 #endif
@@ -318,6 +359,10 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t3);
 #endif
+    if constexpr (PSYNC) {          // (waited for with the next stage's pieces)
+      if (psync_on && (s + 1) % QW_PS_EVERY == 0)
+        ps_seen = __hip_atomic_load(psync + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // ---- epilogue of tile t0 + s: this wave's 32 queries x SR rows ----
     int le;
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));

@@ -14,38 +14,47 @@ using namespace hcr;
 
 namespace {
 
-int qw_dm() {                 // HCRAG_QW_DM (r05 A/B hook, read once): score_qw.h DM
+// The DMA-issue mode (score_qw.h DM) when the index option does not set one: spread over the
+// MFMA groups (3) when the launch has one query block -- every row stage feeds one workgroup, so
+// nothing is lost if workgroups drift apart: 10M x 768 B = 256 3.75 vs 3.88 ms, 1M x 384 B = 256
+// 0.266 vs 0.278 ms score phase (r05c, interleaved in one process, profiles/r05/) -- and every
+// wave at the barrier (0) with several: spread issue lets the query blocks of a row partition
+// drift apart, and FETCH_SIZE grows 2.65x for -0.9 % at the headline (r05b/c; with a
+// partition-sync counter (4) 1.4x and +3 %).  HCRAG_QW_DM (read once) overrides the default.
+int qw_dm(int nqb) {
   static const int v = [] {
     const char* e = getenv("HCRAG_QW_DM");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
-  return v;
+  return v >= 0 ? v : nqb == 1 ? 3 : 0;
 }
 
 template <typename TM, int CAP, int KS, int SR, int NST, int DM>
 void launch_dense(const QsArgs& a, hipStream_t st) {
+  if (DM == 4 && a.psync) (void)hipMemsetAsync(a.psync, 0, (size_t)a.P * 4, st);
   hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, DM>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                      st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr,
+                     DM == 4 ? a.psync : nullptr);
 }
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
 void launch_t(const QsArgs& a, hipStream_t st) {
-  if constexpr (256 % SR != 0) {   // (a dense-only stage shape: the pre-pass never asks for it)
-    switch (qw_dm()) {
-      case 1: launch_dense<TM, CAP, KS, SR, NST, 1>(a, st); break;
-      case 2: launch_dense<TM, CAP, KS, SR, NST, 2>(a, st); break;
-      case 3: launch_dense<TM, CAP, KS, SR, NST, 3>(a, st); break;
-      default: launch_dense<TM, CAP, KS, SR, NST, 0>(a, st);
+  if constexpr (256 % SR == 0) {   // (48-row stages are dense-only: the pre-pass never asks)
+    if (a.umax) {                  // the sampling pre-pass (MAXONLY)
+      hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT),
+                         0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
+                         a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, a.tstride, a.umax);
+      return;
     }
-  } else if (a.umax)       // the sampling pre-pass (MAXONLY)
-    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, true>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
-                       st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, a.tstride, a.umax);
-  else
-    hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST>), dim3(a.nqb * a.P), dim3(V3_NT), 0, st,
-                       static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                       a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+  }
+  switch (a.dm >= 0 ? a.dm : qw_dm(a.nqb)) {
+    case 1: launch_dense<TM, CAP, KS, SR, NST, 1>(a, st); break;
+    case 2: launch_dense<TM, CAP, KS, SR, NST, 2>(a, st); break;
+    case 3: launch_dense<TM, CAP, KS, SR, NST, 3>(a, st); break;
+    case 4: launch_dense<TM, CAP, KS, SR, NST, 4>(a, st); break;
+    default: launch_dense<TM, CAP, KS, SR, NST, 0>(a, st);
+  }
 }
 
 // Dense-pass stage shape at D = 768: 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows

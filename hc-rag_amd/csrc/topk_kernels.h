@@ -904,6 +904,8 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
 //   queries of prep_queries_kernel, 16 per wave: waves 0 / 2 queries 0-15, 1 / 3 queries
 //   16-31), rows stream straight from HBM as A fragments, 16-row tiles; the coarse score is
 //   c = fl(q^.e . inv32) with |c - exact| <= eps_q (the non-UNIT bound).
+//   One launch scans the rows once for up to kFbGroupsPerScan groups (blocks of a row chunk's
+//   groups adjacent on one XCD: the other groups read the rows from L2).
 //   K6m (HIST = false): a (row, query) pair whose c reaches T_q - eps_q -- T_q the score of the
 //   query's threshold key -- gets the fp64 cosine in K6's summation order (a wave per pair:
 //   bit-identical scores), then K6's key test, append and histogram; every row whose exact key
@@ -911,9 +913,14 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
 //   K6h (HIST = true, round 0 when a query has no starting threshold, k > 256): a histogram of
 //   c per query over [-kFbHistRange, kFbHistRange) in kFbHistBins bins, from which the host
 //   takes T_q = (lower edge of the bin where k rows are reached from the top) - eps_q: at least
-//   k rows have c >= edge, hence exact >= T_q, so T_q <= the true k-th best.
+//   k rows have c >= edge, hence exact >= T_q, so T_q <= the true k-th best.  On a large
+//   corpus the histogram covers a sample (hstride > 1: one run of 4 tiles in 4 hstride) and
+//   the edge is where the sample reaches f k + 5 sqrt(f k) + 3 rows (f the sampled fraction):
+//   an ESTIMATED threshold -- if the filter round then admits fewer than k rows, the select
+//   (K7) drops it to "every row" and the round repeats, so the result stays exact.
 // -------------------------------------------------------------------------------------
 constexpr int kFbHistBins = 512;
+constexpr int kFbGroupsPerScan = 4;  // query groups of kFbGroup per MFMA-prefiltered scan
 constexpr float kFbHistRange = 1.0625f;
 
 template <typename TS, int KS, bool HIST>
@@ -928,7 +935,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
                          uint64_t* __restrict__ buf_hi, uint64_t* __restrict__ buf_lo,
                          const double* __restrict__ h_lo, const double* __restrict__ h_hi,
                          unsigned int* __restrict__ h_cnt, unsigned long long* __restrict__ h_min,
-                         unsigned int* __restrict__ c_hist) {
+                         unsigned int* __restrict__ c_hist, int ngroups, int hstride) {
   using Op = MfmaOp<TS>;
   using V = typename Op::V;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
@@ -939,6 +946,13 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   unsigned int (*s_cnt)[kFbBins + 1] = reinterpret_cast<unsigned int (*)[kFbBins + 1]>(sm);
   unsigned long long (*s_min)[kFbBins + 1] =
       reinterpret_cast<unsigned long long (*)[kFbBins + 1]>(sm + (size_t)kFbGroup * (kFbBins + 1) * 4);
+  // block -> (query group, row chunk): the ngroups groups of one row chunk are consecutive
+  // blocks of one XCD (round-robin dispatch), so each row tile comes from HBM once per scan and
+  // from that XCD's L2 for the other groups (the grid is a multiple of 8 x ngroups)
+  const int xcd = blockIdx.x & 7, rr = blockIdx.x >> 3;
+  const int grp = rr % ngroups, chunk = (rr / ngroups) * 8 + xcd;
+  const int nchunks = gridDim.x / ngroups;
+  const int qg0 = grp * kFbGroup, nqg = min(kFbGroup, nq - qg0);
   if constexpr (HIST) {
     for (int i = threadIdx.x; i < kFbGroup * kFbHistBins; i += blockDim.x) s_hist[i] = 0u;
   } else {
@@ -949,7 +963,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     if (threadIdx.x < kFbGroup) {
       const int q = threadIdx.x;
       // the prefilter bound: pairs below it cannot reach the threshold key's score
-      s_tc[q] = (q < nq && active[q]) ? unord64(th_hi[q]) - eps[q] : INFINITY;
+      s_tc[q] = (q < nqg && active[qg0 + q]) ? unord64(th_hi[qg0 + q]) - eps[qg0 + q] : INFINITY;
     }
   }
   __syncthreads();
@@ -959,38 +973,59 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   // query fragments: lane l holds q^[qb*16 + (l & 15)][32 ks + 8 (l >> 4) .. + 8)
   V qf[KS];
   {
-    const TS* src = qhat + (size_t)ql * ld + (lane >> 4) * 8;
+    const TS* src = qhat + (size_t)(qg0 + ql) * ld + (lane >> 4) * 8;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
   }
-  const bool qok = ql < nq && active[ql];
+  const bool qok = ql < nqg && active[qg0 + ql];
   const double tcq = HIST ? 0.0 : s_tc[ql];
   const int64_t ntile = (n + 15) / 16;
-  const int64_t stride = (int64_t)gridDim.x * 2;
-  for (int64_t t = (int64_t)blockIdx.x * 2 + (wave >> 1); t < ntile; t += stride) {
+  const int64_t stride = (int64_t)nchunks * 2;
+  // (HIST: runs of 4 tiles out of every 4 hstride -- a sample of the rows when hstride > 1)
+  auto tile_of = [&](int64_t tv) -> int64_t {
+    return HIST ? (tv >> 2) * (4 * (int64_t)hstride) + (tv & 3) : tv;
+  };
+  // A fragments straight from the rows (the slack rows past n are readable; masked below), in
+  // NB batches of CH k-steps; the next tile's first batch is issued before this tile's epilogue
+  // (after its inv32 / mask loads: vmcnt counts in order), so one tile's load latency hides
+  // behind the previous tile's epilogue (r05: 3 dependent batches per tile, no overlap, ran the
+  // scan at ~3 TB/s)
+  // (KS = 24 in one batch: 262 registers, KS = 32 in 16-deep batches: 264 -- one wave per SIMD)
+  constexpr int CH = KS <= 12 ? KS : KS == 24 ? 12 : 8, NB = (KS + CH - 1) / CH;
+  auto frag_ptr = [&](int64_t t) { return rows + (t * 16 + (lane & 15)) * ld + (lane >> 4) * 8; };
+  V a[CH];
+  auto load_batch = [&](const TS* ra, int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      if (b * CH + j < KS) a[j] = *reinterpret_cast<const V*>(ra + (b * CH + j) * 32);
+  };
+  int64_t tv = (int64_t)chunk * 2 + (wave >> 1);
+  if (tile_of(tv) < ntile) load_batch(frag_ptr(tile_of(tv)), 0);
+  for (;; tv += stride) {
+    const int64_t t = tile_of(tv);
+    if (t >= ntile) break;
     const int64_t r0 = t * 16;
-    // A fragments straight from the rows (the slack rows past n are readable; masked below)
-    const TS* ra = rows + (r0 + (lane & 15)) * ld + (lane >> 4) * 8;
+    const int64_t tn = tile_of(tv + stride);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    constexpr int CH = 8;                            // k-steps per batch of loads in flight
-#pragma unroll
-    for (int k0 = 0; k0 < KS; k0 += CH) {
-      V a[CH];
-#pragma unroll
-      for (int j = 0; j < CH; ++j)
-        if (k0 + j < KS) a[j] = *reinterpret_cast<const V*>(ra + (k0 + j) * 32);
-#pragma unroll
-      for (int j = 0; j < CH; ++j)
-        if (k0 + j < KS) acc = Op::run(a[j], qf[k0 + j], acc);
-    }
     const int64_t rb = r0 + (lane >> 4) * 4;         // the lane's 4 rows: rb .. rb + 3
     float iv[4];
     bool rok[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = rb + r;
-      rok[r] = qok && row < n && (!maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u));
-      iv[r] = row < n ? inv32[row] : 0.f;
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (b * CH + j < KS) acc = Op::run(a[j], qf[b * CH + j], acc);
+      if (b + 1 < NB) {
+        load_batch(frag_ptr(t), b + 1);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = rb + r;
+          rok[r] = qok && row < n && (!maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u));
+          iv[r] = row < n ? inv32[row] : 0.f;
+        }
+        if (tn < ntile) load_batch(frag_ptr(tn), 0);
+      }
     }
     if constexpr (HIST) {
 #pragma unroll
@@ -1009,7 +1044,8 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
         while (m) {                                  // a wave per admitted pair (rare)
           const int src = __builtin_ctzll(m);
           m &= m - 1;
-          const int q = __builtin_amdgcn_readlane(ql, src);
+          const int qs_ = __builtin_amdgcn_readlane(ql, src);    // (group-local)
+          const int q = qg0 + qs_;
           const int64_t row = rb - (lane >> 4) * 4 + (src >> 4) * 4 + r;
           const TS* e = rows + row * ld;
           const float* qs = q32 + (int64_t)q * dim;
@@ -1036,8 +1072,8 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
                 const double tt = (sc - lo) * ((double)kFbBins / (hi - lo));
                 b = tt < 0.0 ? 0 : tt >= (double)(kFbBins - 1) ? kFbBins - 1 : (int)tt;
               }
-              atomicAdd(&s_cnt[q][b], 1u);
-              atomicMin(&s_min[q][b], (unsigned long long)h);
+              atomicAdd(&s_cnt[qs_][b], 1u);
+              atomicMin(&s_min[qs_][b], (unsigned long long)h);
             }
           }
         }
@@ -1046,16 +1082,16 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   }
   __syncthreads();
   if constexpr (HIST) {
-    for (int i = threadIdx.x; i < nq * kFbHistBins; i += blockDim.x) {
+    for (int i = threadIdx.x; i < nqg * kFbHistBins; i += blockDim.x) {
       const unsigned int c = s_hist[i];
-      if (c) atomicAdd(&c_hist[i], c);
+      if (c) atomicAdd(&c_hist[(size_t)qg0 * kFbHistBins + i], c);
     }
   } else {
-    for (int i = threadIdx.x; i < nq * (kFbBins + 1); i += blockDim.x) {
+    for (int i = threadIdx.x; i < nqg * (kFbBins + 1); i += blockDim.x) {
       const unsigned int c = (&s_cnt[0][0])[i];
       if (c) {
-        atomicAdd(&h_cnt[i], c);
-        atomicMin(&h_min[i], (&s_min[0][0])[i]);
+        atomicAdd(&h_cnt[(size_t)qg0 * (kFbBins + 1) + i], c);
+        atomicMin(&h_min[(size_t)qg0 * (kFbBins + 1) + i], (&s_min[0][0])[i]);
       }
     }
   }
@@ -1071,11 +1107,28 @@ exact_select_kernel(int k, int cap, const unsigned int* __restrict__ cnt,
                     const int* __restrict__ out_idx, double* __restrict__ out_s,
                     int64_t* __restrict__ out_i, double* __restrict__ h_lo,
                     double* __restrict__ h_hi, const unsigned int* __restrict__ h_cnt,
-                    const unsigned long long* __restrict__ h_min) {
+                    const unsigned long long* __restrict__ h_min, int* __restrict__ est) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm_sel[];
   const int q = blockIdx.x;
   if (!active[q]) return;
   const unsigned int c = cnt[q];
+  if (est && est[q]) {
+    // an estimated starting threshold (K6h over a sample) that admitted fewer than k rows lies
+    // above the k-th best: the next round admits every row (rare: ~1e-8 per query)
+    if (c < (unsigned int)k) {
+      if (threadIdx.x == 0) {
+        th_hi[q] = 0ull;
+        th_lo[q] = 0ull;
+        h_lo[q] = -1.0 - 1e-6;
+        h_hi[q] = 1.0 + 1e-6;
+        est[q] = 0;
+        atomicAdd(n_again, 1);
+      }
+      return;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) est[q] = 0;       // (>= k rows at or above it: a valid bound from here)
+  }
   const int nload = (int)min(c, (unsigned int)cap);
   int m = 1;
   while (m < nload || m < k) m <<= 1;                  // <= cap (power of two, cap > k)

@@ -188,6 +188,8 @@ class VectorIndex:
     OPT_SAMPLE_STRIDE = 3
     OPT_QS_FORM = 4
     OPT_PREPASS = 5
+    OPT_QW_DM = 6
+    OPT_QW_MIN = 7
 
     def set_option(self, option: int, value: int) -> None:
         """Kernel-choice option (``hcr_index_set_option``); never changes results.
@@ -195,7 +197,9 @@ class VectorIndex:
         ``VectorIndex.OPT_SAMPLE_STRIDE``: the sampling pre-pass's row-tile stride (0 heuristic).
         ``VectorIndex.OPT_QS_FORM``: QS ring stages at D = 384, 129-256 queries: 0 heuristic,
         1 64-deep, 3 128-deep.
-        ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel under QW, 1 v4, 2 QW (0 heuristic)."""
+        ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel, 1 v4, 2 QW (0 heuristic).
+        ``VectorIndex.OPT_QW_DM``: QW's LDS-DMA issue mode, -1 default, 0-4 (hcrag.h).
+        ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
 

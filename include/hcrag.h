@@ -166,10 +166,18 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                a longer pre-pass.
  *   HCR_OPT_QS_FORM: the query-stationary kernel's ring stages for 129-256 queries at D = 384:
  *                0 = the heuristic (= 3), 1 = 64-deep stages, 3 = 128-deep stages.
- *   HCR_OPT_PREPASS: the sampling pre-pass kernel when the dense pass runs on QW: 0 = the
- *                heuristic, 1 = the 256 x 256 v4 kernel's MAXONLY form, 2 = QW's MAXONLY form. */
+ *   HCR_OPT_PREPASS: the sampling pre-pass kernel: 0 = the heuristic, 1 = the 256 x 256 v4
+ *                kernel's MAXONLY form, 2 = QW's MAXONLY form (also under the QS dense pass, on
+ *                an L2-normalised corpus without a row mask).
+ *   HCR_OPT_QW_DM: how the wide query-stationary kernel (QW) issues a row stage's LDS-DMA:
+ *                -1 = the default, 0 = every wave at the stage barrier, 1 = waves 0-3 at the
+ *                barrier, 2 = waves 0-3 spread over their MFMA groups, 3 = every wave spread,
+ *                4 = as 3 with the query blocks of a row partition kept in step.
+ *   HCR_OPT_QW_MIN: the smallest batch the QW kernel takes (0 = the heuristic: 129 at D = 768,
+ *                257 at D = 384). */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,
-               HCR_OPT_PREPASS = 5 } hcr_index_option;     /* (2: removed in 0.3) */
+               HCR_OPT_PREPASS = 5, HCR_OPT_QW_DM = 6, HCR_OPT_QW_MIN = 7 } hcr_index_option;
+               /* (2: removed in 0.3) */
 int hcr_index_set_option(hcr_index* index, int option, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)

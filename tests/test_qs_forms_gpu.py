@@ -46,6 +46,7 @@ def test_qs_form_parity(hc, dtype, D, form, B, k, normalize):
     Q, src = _planted(rng, E, B)
     with hc.VectorIndex(D, dtype) as ix:
         ix.set_option(ix.OPT_QS_FORM, form)
+        ix.set_option(ix.OPT_QW_MIN, 1 << 30)      # (r05: QW takes 129+ queries at D = 384 by default)
         ix.add(E, normalize=normalize)
         R = ix.get_rows()
         s, i = ix.search(Q, k)

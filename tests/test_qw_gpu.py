@@ -42,7 +42,7 @@ def _planted(rng, E, B, noise=0.2, with_src=False):
 
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
 @pytest.mark.parametrize("D", [384, 768])
-@pytest.mark.parametrize("B,k", [(257, 10), (512, 32), (1024, 32), (1100, 64)])
+@pytest.mark.parametrize("B,k", [(130, 10), (256, 10), (257, 10), (512, 32), (1024, 32), (1100, 64)])
 def test_qw_parity(hc, dtype, D, B, k):
     """N not a multiple of the 32 / 64-row stage (the last tile ends past the corpus), several
     hundred tiles per workgroup (the seeded pre-pass runs), padded query blocks (257, 1100)."""
@@ -190,3 +190,26 @@ def test_qw_maxonly_prepass_forms_agree(hc, D, N):
     sub = np.r_[0:12, B - 12:B]
     es, ei = O.cosine_topk(Q[sub], R, k)
     _check(out[2][0][sub], out[2][1][sub], es, ei)
+
+
+@pytest.mark.parametrize("D", [384, 768])
+def test_qw_dma_modes_agree(hc, D):
+    """Every stage DMA-issue mode of QW (HCR_OPT_QW_DM 0-4: at the barrier, waves 0-3 only,
+    spread over the MFMA groups, with the partition-sync counter) on one index, one and four
+    query blocks: ids identical to the oracle and to each other."""
+    rng = np.random.default_rng(D + 3)
+    N = 90000 + 13
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        for B in (200, 1024):
+            Q = _planted(rng, E, B)
+            sub = np.r_[0:16, B - 16:B]
+            es, ei = O.cosine_topk(Q[sub], R, 16)
+            for dm in (0, 1, 2, 3, 4, -1):
+                ix.set_option(ix.OPT_QW_DM, dm)
+                s, i = ix.search(Q, 16)
+                st = ix.last_stats()
+                assert st["score_kernel"] == QW and st["uncertified_queries"] == 0, (dm, st)
+                _check(s[sub], i[sub], es, ei)

@@ -1,7 +1,7 @@
 """Where the QW score kernel's dense launch spends a stage, from the stamps build (Makefile target
 `stamps_qw`):
 
-    HCRAG_LIB=hc-rag_amd/lib/stamps_qw/libhcrag_hip.so python tools/qw_stamps.py ROWS DIM BATCH
+    HCRAG_LIB=hc-rag_amd/lib/stamps_qw/libhcrag_hip.so python tools/qw_stamps.py ROWS DIM BATCH [K] [OPT=V ...]
 
 Runs a few searches on a synthetic L2-normalised corpus, then reads the per-wave s_memtime sums
 of the last dense QW launch: stage wait (vmcnt + barrier), DMA issue + bound reads, MFMA groups
@@ -22,12 +22,16 @@ import hcrag_amd  # noqa: E402
 from hcrag_amd import _lib  # noqa: E402
 
 N, D, B = (int(x) for x in sys.argv[1:4])
+K = int(sys.argv[4]) if len(sys.argv) > 4 else 32
 dev = torch.device("cuda:0")
 ix = hcrag_amd.VectorIndex(D, "f16", device=0, capacity=N)
 bench.make_shard(ix, hcrag_amd, 0, N, D, "f16", dev)
+for kv in sys.argv[5:]:                    # index options NAME=VALUE (VectorIndex.OPT_NAME)
+    name, v = kv.split("=")
+    ix.set_option(getattr(ix, "OPT_" + name), int(v))
 Q = np.random.default_rng(1).standard_normal((B, D)).astype(np.float32)
 for _ in range(3):
-    ix.search(Q, 32)
+    ix.search(Q, K)
 st = ix.last_stats()
 fn = _lib.lib().hcr_debug_qw_stamps
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
