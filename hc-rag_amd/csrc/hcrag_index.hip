@@ -533,6 +533,7 @@ struct TestHooks {
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
   bool no_finish = false;            // HCRAG_NO_FINISH: separate merge + rescore launches
   bool no_mfma_filter = false;       // HCRAG_NO_MFMA_FILTER: the fallback's scans on K6 (fp64 only)
+  bool seed_from_kp = false;         // HCRAG_SEED_FROM_KP: the seed rank from k' (r04) instead of k
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -546,6 +547,7 @@ static const TestHooks& hooks() {
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
     t.no_mfma_filter = getenv("HCRAG_NO_MFMA_FILTER") != nullptr;
+    t.seed_from_kp = getenv("HCRAG_SEED_FROM_KP") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -1073,9 +1075,14 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       V3Launch a{nqb_pre, 0, (int)((ntiles_pre + stride - 1) / stride), stride, kp, unit};
       a.P = std::max(1, std::min(a.nvt, (wg_target + nqb_pre - 1) / nqb_pre));
       a.P = std::min(a.P, P);                  // partials / merge buffers are sized for P
+      // r05: lambda counts the sample's expected share of the global top-k, not top-k': the
+      // seed only has to leave >= k rows above it for the short-list certificate (B = tau_est,
+      // DESIGN.md §4), and a lower j halves the dense pass's appends where k' >> k (configs[1]:
+      // k = 10, k' = 64, stride 16: j 17 -> 8).  HCRAG_SEED_FROM_KP restores lambda = k' x f.
       int j = kp;
       if (!rigorous_seed && !th.rigorous_seed) {
-        const double lam = (double)kp * ((double)a.nvt * tr_pre) / (double)ix->n;
+        const int kseed = th.seed_from_kp ? kp : k;
+        const double lam = (double)kseed * ((double)a.nvt * tr_pre) / (double)ix->n;
         j = th.seed_rank ? th.seed_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
         j = std::min(kp, std::max(1, j));
       }

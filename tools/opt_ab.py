@@ -79,8 +79,8 @@ for r in range(R):
         ix.set_timing(False)
         st = ix.last_stats()
         res[a].append((wall, km / n))
-        print(f"round {r} {a:40s} wall {wall:.4f} ms  score {km / n:.4f} ms  kernel {st['score_kernel']}",
-              flush=True)
+        print(f"round {r} {a:40s} wall {wall:.4f} ms  score {km / n:.4f} ms  kernel {st['score_kernel']}"
+              f"  widened {st['widened_queries']}  fallback {st['fallback_queries']}", flush=True)
 print(f"== {N} x {D}, B = {B}, k = {K}: medians over {R} rounds")
 for a in arms:
     w = np.median([x[0] for x in res[a]])
