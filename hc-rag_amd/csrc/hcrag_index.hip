@@ -57,7 +57,7 @@ struct hcr_index {
   hipStream_t stream = nullptr;
   // search workspace
   DevBuf w_qin, w_qhat, w_qnorm, w_eps, w_taug, w_buf, w_part, w_merged, w_outs, w_outi,
-      w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt, w_psync;
+      w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
       f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est;
@@ -137,7 +137,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_qin, &ix->w_qhat, &ix->w_qnorm, &ix->w_eps, &ix->w_taug,
                    &ix->w_buf, &ix->w_part, &ix->w_merged, &ix->w_outs, &ix->w_outi,
                    &ix->w_unc, &ix->w_cnt, &ix->w_tauest, &ix->w_umax, &ix->w_sk,
-                   &ix->w_pcnt, &ix->w_mcnt, &ix->w_psync,
+                   &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
                    &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est};
@@ -437,7 +437,8 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       ix->opt_prepass = value;
       return HCR_OK;
     case HCR_OPT_QW_DM:
-      if (value < -1 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_QW_DM value %d not in [-1, 4]", value);
+      if (value != -1 && value != 0 && value != 3)
+        return set_err(HCR_EINVAL, "HCR_OPT_QW_DM value %d not -1, 0 or 3", value);
       ix->opt_qw_dm = value;
       return HCR_OK;
     case HCR_OPT_QW_MIN:
@@ -683,8 +684,6 @@ static int launch_qw_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
   QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, a.nqb,
            a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
-  CHECK(ix->w_psync.ensure((size_t)std::max(a.P, 1) * 4));
-  q.psync = ix->w_psync.as<uint32_t>();
   q.dm = ix->opt_qw_dm;
   return launch_qw(ix->dtype, q, st);
 }

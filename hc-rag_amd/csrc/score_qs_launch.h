@@ -23,8 +23,8 @@ struct QsArgs {
                              // KS = 12)
   float* umax = nullptr;     // QW: the MAXONLY sampling pre-pass into umax[unit][nqb * 256]
                              // (ntiles = virtual stages of the sampled tiles, tstride their stride)
-  uint32_t* psync = nullptr; // QW dense pass: one arrival counter per row partition (P words)
-  int dm = -1;               // QW dense pass: DMA-issue mode (score_qw.h DM; -1 = the default)
+  int dm = -1;               // QW dense pass: stage DMA issue, 0 at the barrier, 3 spread over
+                             // the MFMA groups, -1 the default (score_qw.h SPREAD)
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128

@@ -47,8 +47,6 @@ __device__ unsigned long long hcr_qw_stamps[4096 * 8 * 8];
 
 constexpr int QW_QT = 256;      // queries per workgroup (8 waves x 32; kQwQueries on the host)
 constexpr int QW_NST = 3;       // ring stages
-constexpr int QW_PS_EVERY = 2;  // DM 4: stages per partition sync point
-constexpr int QW_PS_LAG = 1;    // ... sync points a workgroup may run ahead of its slowest sibling
 
 // rows per stage for KS 32-deep k-steps: 48 KiB stages (RB = SR / 16 row blocks, even)
 constexpr int qw_sr(int ks) { return ks == 24 ? 32 : ks == 12 ? 64 : 0; }
@@ -107,31 +105,26 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
 // stages of the sampled 256-row tiles (tile vt * tstride, 256 / SR stages each), partitions are
 // whole 128-row units, and per unit and query the largest coarse score goes to
 // umax[unit][nqb * QT] -- no candidate lists (v4's MAXONLY form is LDS-fill-bound).
-// DM: who issues a stage's LDS-DMA ops and when.  0: every wave its PPW pieces + its bounds,
-// all right after the stage barrier; 1: waves 0-3 only (2 PPW pieces + two waves' bounds each),
-// right after the barrier -- waves 4-7 go straight to their MFMAs; 2: waves 0-3 only, one op
-// per GSTEP MFMA groups over the first 3/4 of them; 3: every wave, spread likewise; 4: as 3, and
-// the nqb workgroups of a row partition (the query blocks that share each row stage through
-// their XCD's L2) kept within QW_PS_LAG sync points of each other by an arrival counter per
-// partition (psync[p], zeroed per launch): spread issue alone lets them drift apart and the row
-// stages are fetched from HBM once per query block instead of once (r05b: FETCH_SIZE 2.65x).
+// SPREAD: when a stage's LDS-DMA ops are issued.  false: every wave its PPW pieces + its bounds
+// right after the stage barrier; true: one op every GSTEP MFMA groups over the first 3/4 of the
+// wave's groups (r05, DESIGN.md §5.2: 8 % fewer cycles per stage; the default with one query
+// block -- with several, the query blocks of a row partition drift apart and each row stage
+// is fetched from HBM once per block).  r05 also measured, and removed: waves 0-3 issuing every
+// op (at the barrier or spread), a per-partition arrival counter keeping the query blocks in
+// step, and LDS ready / done counters in place of the stage barrier (profiles/r05/).
 template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false,
-          int DM = 0>
+          bool SPREAD = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
                      uint64_t* __restrict__ buf, uint32_t* __restrict__ tau_g,
                      uint64_t* __restrict__ partials, int* __restrict__ pcnt, int kp,
-                     int tstride = 1, float* __restrict__ umax = nullptr,
-                     uint32_t* __restrict__ psync = nullptr) {
+                     int tstride = 1, float* __restrict__ umax = nullptr) {
   using L = QwLayout<KS, SR_, NST_>;
   using Op = MfmaOp<TM>;
   using V = typename Op::V;
   constexpr int SR = L::SR, RB = L::RB, PPW = L::PPW, QT = QW_QT, NST = L::NST, D = NST - 1;
-  // issuing waves, pieces per issuing wave, vmcnt-counted ops per issuing wave per stage
-  constexpr int NIW = (DM == 1 || DM == 2) ? 4 : 8, PPI = L::PIECES / NIW, OPS = PPI + 8 / NIW;
-  constexpr bool SPREAD = DM >= 2, PSYNC = DM == 4 && !MAXONLY;
-  static_assert(L::PIECES % NIW == 0, "pieces per issuing wave");
+  constexpr int OPS = PPW + 1;                       // vmcnt-counted ops per wave per stage
   // fragment groups per stage: (row-block pair, k-step) for the row-block pairs, then (the odd
   // last row block, k-step pair) when RB is odd
   constexpr int NGP = (RB / 2) * KS, NG = NGP + (RB % 2) * (KS / 2);
@@ -202,10 +195,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                                             0x00020000);
     return d;
   };
-  const bool issuer = NIW == 8 || wave < NIW;
   auto issue_op = [&](const StageDesc& d, int u) __attribute__((always_inline)) {
-    if (u < PPI) {
-      const int j = wave + NIW * u;
+    if (u < PPW) {
+      const int j = wave + 8 * u;
       // the piece's source offset re-derived per stage from an opaque copy of the row pitch:
       // hoisted, the PPW offsets hold PPW SGPRs across the loop (48-row stages: SGPR spills)
       int ldbs = ldb;
@@ -217,18 +209,16 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       int tv;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\t"
                    "v_and_b32 %0, 31, %0\n\tv_lshlrev_b32 %0, 2, %0" : "=v"(tv));
-      const int bw = wave + NIW * (u - PPI);          // the wave whose 32 bounds these are
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * 8 + bw) * 256),
-          4, tv, bw * 32 * 4, 0, 0);
+          d.t, (__attribute__((address_space(3))) void*)(lds + L::TGS + (d.slot * 8 + wave) * 256),
+          4, tv, wq0 * 4, 0, 0);
     }
   };
-  if (issuer)
-    for (int i = 0; i < D; ++i) {
-      const StageDesc d = stage_desc(i);
+  for (int i = 0; i < D; ++i) {
+    const StageDesc d = stage_desc(i);
 #pragma unroll
-      for (int u = 0; u < OPS; ++u) issue_op(d, u);
-    }
+    for (int u = 0; u < OPS; ++u) issue_op(d, u);
+  }
 
   const uint32_t offA = (uint32_t)((lane & 15) * 64 + v3_slot(lane >> 4, lane & 15) * 16);
   const uint32_t lds0 = lds_addr(lds);
@@ -238,47 +228,14 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   float umx[2] = {0.f, 0.f};                         // MAXONLY: the current unit's maxima
 #ifdef HCR_QW_STAMPS
   uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
+  const uint64_t st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  // DM 4: the partition's arrival count, loaded one stage ahead of its check (wave 0)
-  const bool psync_on = PSYNC && psync != nullptr && nqb > 1 && wave == 0;
-  uint32_t ps_seen = 0;
-  int ps_budget = 1 << 14;           // total spins before this workgroup stops waiting (a sibling
-                                     // not resident -- never the case at one workgroup per CU)
   for (int s = 0; s < nsteps; ++s) {
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t0);
 #endif
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
-    if constexpr (PSYNC) {
-      if (psync_on && s % QW_PS_EVERY == 0 && s / QW_PS_EVERY > QW_PS_LAG) {
-        const uint32_t target = (uint32_t)nqb * (uint32_t)(s / QW_PS_EVERY - QW_PS_LAG);
-        if (__builtin_amdgcn_readfirstlane(ps_seen) < target && ps_budget > 0) {
-          // the bounded spin as one asm block (a compiler-visible loop here spilled the query
-          // fragments): sc1 loads of the counter, s_sleep between them
-          uint32_t v;
-          asm volatile(
-              "1:\n\t"
-              "s_sleep 2\n\t"
-              "global_load_dword %[v], %[a], off sc1\n\t"
-              "s_waitcnt vmcnt(0)\n\t"
-              "v_readfirstlane_b32 %[t], %[v]\n\t"
-              "s_sub_u32 %[b], %[b], 1\n\t"
-              "s_cmp_ge_u32 %[t], %[g]\n\t"
-              "s_cbranch_scc1 2f\n\t"
-              "s_cmp_gt_i32 %[b], 0\n\t"
-              "s_cbranch_scc1 1b\n"
-              "2:"
-              : [v] "=&v"(v), [t] "=&s"(ps_seen), [b] "+s"(ps_budget)
-              : [a] "v"(psync + p), [g] "s"(target)
-              : "memory", "scc");
-        }
-      }
-    }
     v3_barrier();                  // everyone's pieces of stage s; everyone done with slot s-1
-    if constexpr (PSYNC) {
-      if (psync_on && s % QW_PS_EVERY == 0 && __builtin_amdgcn_mbcnt_lo(~0u, 0) == 0)
-        __hip_atomic_fetch_add(psync + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t1);
 #endif
@@ -286,11 +243,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     // MFMA groups they cost 10 % fewer wave cycles but the 4 query blocks of a row partition
     // drifted apart and FETCH_SIZE grew 2.6x (their shared L2 reuse broken: DESIGN.md §5)
     if constexpr (!SPREAD) {
-      if (issuer) {
-        const StageDesc nd = stage_desc(s + D);
+      const StageDesc nd = stage_desc(s + D);
 #pragma unroll
-        for (int u = 0; u < OPS; ++u) issue_op(nd, u);
-      }
+      for (int u = 0; u < OPS; ++u) issue_op(nd, u);
     }
     [[maybe_unused]] const StageDesc nd = SPREAD ? stage_desc(s + D) : StageDesc{};
 
@@ -328,7 +283,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
       if constexpr (SPREAD) {       // op u at group u * GSTEP (folds to constants when unrolled)
-        if (j % GSTEP == 0 && j / GSTEP < OPS && issuer) issue_op(nd, j / GSTEP);
+        if (j % GSTEP == 0 && j / GSTEP < OPS) issue_op(nd, j / GSTEP);
       }
       if (j + FD - 1 < NG) {
         issue(j + FD - 1, av[(j + FD - 1) % FD]);
@@ -359,10 +314,6 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t3);
 #endif
-    if constexpr (PSYNC) {          // (waited for with the next stage's pieces)
-      if (psync_on && (s + 1) % QW_PS_EVERY == 0)
-        ps_seen = __hip_atomic_load(psync + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     // ---- epilogue of tile t0 + s: this wave's 32 queries x SR rows ----
     int le;
     asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
@@ -470,6 +421,8 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   if (!MAXONLY && lane == 0 && b < 4096) {
     unsigned long long* o = hcr_qw_stamps + ((size_t)b * 8 + wave) * 8;
     o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = st_acc[3]; o[4] = nsteps;
+    o[5] = __builtin_amdgcn_s_memtime() - st_c0;          // shader cycles over the loop ...
+    o[6] = __builtin_amdgcn_s_memrealtime() - st_r0;      // ... and 100 MHz ticks: the clock
   }
 #endif
 

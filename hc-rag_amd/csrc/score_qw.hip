@@ -14,28 +14,26 @@ using namespace hcr;
 
 namespace {
 
-// The DMA-issue mode (score_qw.h DM) when the index option does not set one: spread over the
-// MFMA groups (3) when the launch has one query block -- every row stage feeds one workgroup, so
-// nothing is lost if workgroups drift apart: 10M x 768 B = 256 3.75 vs 3.88 ms, 1M x 384 B = 256
-// 0.266 vs 0.278 ms score phase (r05c, interleaved in one process, profiles/r05/) -- and every
-// wave at the barrier (0) with several: spread issue lets the query blocks of a row partition
-// drift apart, and FETCH_SIZE grows 2.65x for -0.9 % at the headline (r05b/c; with a
-// partition-sync counter (4) 1.4x and +3 %).  HCRAG_QW_DM (read once) overrides the default.
-int qw_dm(int nqb) {
-  static const int v = [] {
+// Stage DMA issue spread over the MFMA groups (score_qw.h SPREAD) when the index option does not
+// choose: with one query block -- every row stage feeds one workgroup, nothing is lost if
+// workgroups drift apart: 10M x 768 B = 256 3.75 vs 3.88 ms, 1M x 384 B = 256 0.266 vs 0.278 ms
+// score phase (r05c, interleaved in one process, profiles/r05/) -- and at the barrier with
+// several: spread issue lets the query blocks of a row partition drift apart, and FETCH_SIZE
+// grows 2.65x for -0.9 % at the headline (r05b/c).  HCRAG_QW_DM (0 / 3, read once) overrides.
+bool qw_spread(int dm, int nqb) {
+  static const int env = [] {
     const char* e = getenv("HCRAG_QW_DM");
     return e ? atoi(e) : -1;
   }();
-  return v >= 0 ? v : nqb == 1 ? 3 : 0;
+  const int m = dm >= 0 ? dm : env >= 0 ? env : (nqb == 1 ? 3 : 0);
+  return m == 3;
 }
 
-template <typename TM, int CAP, int KS, int SR, int NST, int DM>
+template <typename TM, int CAP, int KS, int SR, int NST, bool SPREAD>
 void launch_dense(const QsArgs& a, hipStream_t st) {
-  if (DM == 4 && a.psync) (void)hipMemsetAsync(a.psync, 0, (size_t)a.P * 4, st);
-  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, DM>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
+  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, SPREAD>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
                      st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp, 1, nullptr,
-                     DM == 4 ? a.psync : nullptr);
+                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
@@ -48,13 +46,8 @@ void launch_t(const QsArgs& a, hipStream_t st) {
       return;
     }
   }
-  switch (a.dm >= 0 ? a.dm : qw_dm(a.nqb)) {
-    case 1: launch_dense<TM, CAP, KS, SR, NST, 1>(a, st); break;
-    case 2: launch_dense<TM, CAP, KS, SR, NST, 2>(a, st); break;
-    case 3: launch_dense<TM, CAP, KS, SR, NST, 3>(a, st); break;
-    case 4: launch_dense<TM, CAP, KS, SR, NST, 4>(a, st); break;
-    default: launch_dense<TM, CAP, KS, SR, NST, 0>(a, st);
-  }
+  if (qw_spread(a.dm, a.nqb)) launch_dense<TM, CAP, KS, SR, NST, true>(a, st);
+  else launch_dense<TM, CAP, KS, SR, NST, false>(a, st);
 }
 
 // Dense-pass stage shape at D = 768: 48 rows (72 KiB) in a 2-deep ring -- one barrier per 48 rows

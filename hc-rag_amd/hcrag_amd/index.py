@@ -198,7 +198,7 @@ class VectorIndex:
         ``VectorIndex.OPT_QS_FORM``: QS ring stages at D = 384, 129-256 queries: 0 heuristic,
         1 64-deep, 3 128-deep.
         ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel, 1 v4, 2 QW (0 heuristic).
-        ``VectorIndex.OPT_QW_DM``: QW's LDS-DMA issue mode, -1 default, 0-4 (hcrag.h).
+        ``VectorIndex.OPT_QW_DM``: QW's stage LDS-DMA issue, -1 default, 0 at the barrier, 3 spread.
         ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 

@@ -170,9 +170,9 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                kernel's MAXONLY form, 2 = QW's MAXONLY form (also under the QS dense pass, on
  *                an L2-normalised corpus without a row mask).
  *   HCR_OPT_QW_DM: how the wide query-stationary kernel (QW) issues a row stage's LDS-DMA:
- *                -1 = the default, 0 = every wave at the stage barrier, 1 = waves 0-3 at the
- *                barrier, 2 = waves 0-3 spread over their MFMA groups, 3 = every wave spread,
- *                4 = as 3 with the query blocks of a row partition kept in step.
+ *                -1 = the default (3 with one 256-query block, else 0), 0 = right after the
+ *                stage barrier, 3 = spread over the MFMA groups.  (1, 2, 4, 5: measured in r05,
+ *                removed.)
  *   HCR_OPT_QW_MIN: the smallest batch the QW kernel takes (0 = the heuristic: 129 at D = 768,
  *                257 at D = 384). */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,

@@ -40,7 +40,10 @@ buf = (ctypes.c_ulonglong * n)()
 assert fn(buf, n) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8, 8).astype(np.float64)
 parts = ["wait+barrier", "dma+bounds", "mfma groups", "epilogue"]
-print(f"score_kernel {st['score_kernel']} workgroups {st['workgroups']}")
+live0 = a[:, :, 6] > 0
+ghz = np.median(a[:, :, 5][live0] / a[:, :, 6][live0]) * 0.1 if live0.any() else 0.0
+print(f"score_kernel {st['score_kernel']} workgroups {st['workgroups']}  in-kernel clock {ghz:.3f} GHz "
+      f"(median over waves: s_memtime / s_memrealtime)")
 for name, sel in (("all waves", slice(0, 8)), ("waves 0-3", slice(0, 4)), ("waves 4-7", slice(4, 8))):
     sub = a[:, sel, :]
     live = sub[:, :, 4] > 0
