@@ -68,6 +68,7 @@ struct hcr_index {
   int opt_prepass = 0;          // HCR_OPT_PREPASS (0: the heuristic)
   int opt_qw_dm = -1;           // HCR_OPT_QW_DM (-1: the default)
   int opt_qw_min = 0;           // HCR_OPT_QW_MIN (0: the heuristic)
+  int opt_qw_stagger = -1;      // HCR_OPT_QW_STAGGER (-1: the default)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -441,6 +442,10 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
         return set_err(HCR_EINVAL, "HCR_OPT_QW_DM value %d not -1, 0 or 3", value);
       ix->opt_qw_dm = value;
       return HCR_OK;
+    case HCR_OPT_QW_STAGGER:
+      if (value < -1 || value > 1) return set_err(HCR_EINVAL, "HCR_OPT_QW_STAGGER value %d not in [-1, 1]", value);
+      ix->opt_qw_stagger = value;
+      return HCR_OK;
     case HCR_OPT_QW_MIN:
       if (value < 0) return set_err(HCR_EINVAL, "HCR_OPT_QW_MIN value %d negative", value);
       ix->opt_qw_min = value;
@@ -685,6 +690,7 @@ static int launch_qw_ix(hcr_index* ix, V3Launch a, int cap, hipStream_t st) {
            a.P, a.nvt, 1, ix->w_buf.as<uint64_t>(), ix->w_taug.as<uint32_t>(),
            ix->w_part.as<uint64_t>(), ix->w_pcnt.as<int>(), a.kp, cap, true, 0};
   q.dm = ix->opt_qw_dm;
+  q.stagger = ix->opt_qw_stagger;
   return launch_qw(ix->dtype, q, st);
 }
 

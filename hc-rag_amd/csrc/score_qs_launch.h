@@ -25,6 +25,8 @@ struct QsArgs {
                              // (ntiles = virtual stages of the sampled tiles, tstride their stride)
   int dm = -1;               // QW dense pass: stage DMA issue, 0 at the barrier, 3 spread over
                              // the MFMA groups, -1 the default (score_qw.h SPREAD)
+  int stagger = -1;          // QW dense pass at D = 384: 1 = waves 4-7 run their epilogue one
+                             // stage late (score_qw.h STG), 0 = off, -1 = the default
 };
 
 // True when a kernel is instantiated for this row stride and query blocks per wave (1: 128

@@ -112,8 +112,14 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
 // is fetched from HBM once per block).  r05 also measured, and removed: waves 0-3 issuing every
 // op (at the barrier or spread), a per-partition arrival counter keeping the query blocks in
 // step, and LDS ready / done counters in place of the stage barrier (profiles/r05/).
+// STG (r05, 64-row stages at D = 384 only -- its accumulators fit twice): waves 4-7 run each
+// stage's epilogue one stage late, right after the next stage barrier, so that the epilogue of
+// one wave of a SIMD overlaps the MFMAs of the other (MI355X_MICROARCH.md 'Two waves per SIMD'
+// item 9): waves 0-3 -- first in issue priority -- otherwise finish their MFMAs early, run their
+// epilogue, and wait ~2.4k cycles per stage at the barrier for waves 4-7, whose epilogue then
+// runs with the MFMA pipe idle.
 template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false,
-          bool SPREAD = false>
+          bool SPREAD = false, bool STG = false>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
@@ -230,6 +236,159 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
   const uint64_t st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
+  if constexpr (STG) {
+    static_assert(!MAXONLY, "STG: dense pass only");
+    const bool late = wave >= 4;                     // waves 4-7: the epilogue one stage late
+    constexpr int FD = RB > 2 ? 2 : 3;
+    // the MFMA groups of stage s into acc (and the spread DMA ops of stage s + D)
+    auto mfma_stage = [&](floatx4 (&acc)[RB][2], uint32_t st, const StageDesc& nd, uint32_t (&tg)[2])
+        __attribute__((always_inline)) {
+#pragma unroll
+      for (int m = 0; m < RB; ++m) acc[m][0] = acc[m][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      auto gbase = [&](int j) {
+        return st + (uint32_t)((j < NGP ? 2 * (j / KS) * KS + j % KS : (RB - 1) * KS + 2 * (j - NGP)) * 1024);
+      };
+      auto issue = [&](int j, V (&dst)[2]) __attribute__((always_inline)) {
+        if (j < NGP) qw_issue_frags<KS, V>(gbase(j), offA, dst);
+        else qw_issue_frags<1, V>(gbase(j), offA, dst);
+      };
+      V av[FD][2];
+#pragma unroll
+      for (int j = 0; j < FD - 1; ++j) issue(j, av[j]);
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        if constexpr (SPREAD) {
+          if (j % GSTEP == 0 && j / GSTEP < OPS) issue_op(nd, j / GSTEP);
+        }
+        if (j + FD - 1 < NG) {
+          issue(j + FD - 1, av[(j + FD - 1) % FD]);
+          qw_frag_wait<2 * (FD - 1)>(av[j % FD]);
+        } else if (j + 1 < NG) {
+          qw_frag_wait<2>(av[j % FD]);
+        } else {
+          qw_frag_wait<0>(av[j % FD]);
+          asm volatile("" : "+v"(tg[0]), "+v"(tg[1]));
+        }
+        if (j >= NGP) {
+          const int i = j - NGP;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[RB - 1][n] = Op::run(av[j % FD][kk], qf[n][2 * i + kk], acc[RB - 1][n]);
+        } else {
+          const int m0 = 2 * (j / KS), k0 = j % KS;
+#pragma unroll
+          for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[m0 + mm][n] = Op::run(av[j % FD][mm], qf[n][k0], acc[m0 + mm][n]);
+        }
+      }
+    };
+    // the per-stage test and appends of stage s (as the loop below)
+    auto epilogue = [&](floatx4 (&acc)[RB][2], int s, const uint32_t (&tg)[2]) __attribute__((always_inline)) {
+      int le;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
+      const int lq = le >> 4;
+      const int qle = wq0 + (le & 15);
+      const int64_t row0 = real_stage(t0 + s) * SR;
+      const uint32_t nr32 = (uint32_t)n_rows;
+      if (nr32 < (uint32_t)SR || (uint32_t)row0 > nr32 - (uint32_t)SR) {
+#pragma unroll
+        for (int m = 0; m < RB; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (row0 + m * 16 + lq * 4 + r >= n_rows) acc[m][0][r] = acc[m][1][r] = __builtin_nanf("");
+      }
+      bool hit[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        float mx = qw_max4(acc[0][n]);
+#pragma unroll
+        for (int m = 1; m < RB; ++m) mx = qw_max3(mx, qw_max3(acc[m][n][0], acc[m][n][1], acc[m][n][2]), acc[m][n][3]);
+        hit[n] = qw_ord32(mx) >= max((uint32_t)(tkr[n] >> 32), tg[n]);
+      }
+      if (__any(hit[0] || hit[1])) {
+        float thr[2];
+        thr[0] = unord32(max((uint32_t)(tkr[0] >> 32), tg[0]));
+        thr[1] = unord32(max((uint32_t)(tkr[1] >> 32), tg[1]));
+        const uint32_t row0u = (uint32_t)row0;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          if (!__any(hit[n])) continue;
+#pragma unroll
+          for (int m = 0; m < RB; ++m) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float sc = acc[m][n][r];
+              const bool c = sc >= thr[n];
+              if (__builtin_amdgcn_ballot_w64(c)) {
+                if (c) {
+                  const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
+                  if (key > tkr[n]) {
+                    const int ql = qle + 16 * n;
+                    const int pos = v3_lds_add_rtn(&cnt[ql], 1);
+                    wbuf[(size_t)ql * CAP + pos] = key;
+                    need |= pos + 1 > CAP - SR;
+                  }
+                }
+              }
+            }
+          }
+        }
+        if (__any(need)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+          for (int ql = wq0; ql < wq0 + 32; ++ql) {
+            if ((int)v3_lds_u32(cnt + ql) > CAP - SR)
+              compact_query<CAP>(wbuf + (size_t)ql * CAP, &cnt[ql], &tau_key[ql],
+                                 tau_g + qbase + ql, kp, lane, nullptr);
+          }
+          need = false;
+          tkr[0] = v3_lds_u64(tau_key + qle);
+          tkr[1] = v3_lds_u64(tau_key + qle + 16);
+        }
+      }
+    };
+    // one stage: acc / tg this stage's, pacc / ptg the previous stage's (late waves)
+    auto stage = [&](int s, floatx4 (&acc)[RB][2], uint32_t (&tg)[2], floatx4 (&pacc)[RB][2],
+                     uint32_t (&ptg)[2]) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(OPS * (D - 1)) : "memory");
+      v3_barrier();
+      if constexpr (!SPREAD) {
+        const StageDesc nd = stage_desc(s + D);
+#pragma unroll
+        for (int u = 0; u < OPS; ++u) issue_op(nd, u);
+      }
+      [[maybe_unused]] const StageDesc nd = SPREAD ? stage_desc(s + D) : StageDesc{};
+      const int slot = s % NST;
+      const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + (uint32_t)(slot * L::STAGE)));
+      {
+        int le0;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(le0) : "v"(lane));
+        const uint32_t ta = lds_addr(lds + L::TGS + (slot * 8 + wave) * 256 + (le0 & 15) * 4);
+        asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:64"
+                     : "=&v"(tg[0]), "=&v"(tg[1]) : "v"(ta) : "memory");
+      }
+      if (late && s > 0) epilogue(pacc, s - 1, ptg);
+      mfma_stage(acc, st, nd, tg);
+      if (!late) epilogue(acc, s, tg);
+    };
+    floatx4 acc0[RB][2], acc1[RB][2];
+    uint32_t tg0[2] = {0u, 0u}, tg1[2] = {0u, 0u};
+    int s = 0;
+    for (; s + 1 < nsteps; s += 2) {
+      stage(s, acc0, tg0, acc1, tg1);
+      stage(s + 1, acc1, tg1, acc0, tg0);
+    }
+    if (s < nsteps) stage(s, acc0, tg0, acc1, tg1);
+    if (late) {                                      // the last stage's epilogue
+      if (nsteps % 2) epilogue(acc0, nsteps - 1, tg0);
+      else epilogue(acc1, nsteps - 1, tg1);
+    }
+  } else
   for (int s = 0; s < nsteps; ++s) {
 #ifdef HCR_QW_STAMPS
     if constexpr (!MAXONLY) HCR_QW_STAMP(st_t0);

@@ -29,11 +29,12 @@ bool qw_spread(int dm, int nqb) {
   return m == 3;
 }
 
-template <typename TM, int CAP, int KS, int SR, int NST, bool SPREAD>
+template <typename TM, int CAP, int KS, int SR, int NST, bool SPREAD, bool STG = false>
 void launch_dense(const QsArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, SPREAD>), dim3(a.nqb * a.P), dim3(V3_NT), 0,
-                     st, static_cast<const TM*>(a.rows), a.ld, a.n_rows, static_cast<const TM*>(a.qhat),
-                     a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials, a.pcnt, a.kp);
+  hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, SPREAD, STG>), dim3(a.nqb * a.P),
+                     dim3(V3_NT), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows,
+                     static_cast<const TM*>(a.qhat), a.nqb, a.P, a.ntiles, a.buf, a.tau_g, a.partials,
+                     a.pcnt, a.kp);
 }
 
 template <typename TM, int CAP, int KS, int SR = qw_sr(KS), int NST = QW_NST>
@@ -46,7 +47,18 @@ void launch_t(const QsArgs& a, hipStream_t st) {
       return;
     }
   }
-  if (qw_spread(a.dm, a.nqb)) launch_dense<TM, CAP, KS, SR, NST, true>(a, st);
+  const bool spread = qw_spread(a.dm, a.nqb);
+  // STG: D = 384 only (two accumulator sets fit); on by default -- r05k interleaved A/B on one
+  // box, score phase: 1M x 384 B = 256 0.2277 -> 0.2257 ms, B = 1024 0.7654 -> 0.7455 ms
+  // (profiles/r05/r05k/)
+  if constexpr (KS == 12) {
+    if (a.stagger != 0) {
+      if (spread) launch_dense<TM, CAP, KS, SR, NST, true, true>(a, st);
+      else launch_dense<TM, CAP, KS, SR, NST, false, true>(a, st);
+      return;
+    }
+  }
+  if (spread) launch_dense<TM, CAP, KS, SR, NST, true>(a, st);
   else launch_dense<TM, CAP, KS, SR, NST, false>(a, st);
 }
 

@@ -190,6 +190,7 @@ class VectorIndex:
     OPT_PREPASS = 5
     OPT_QW_DM = 6
     OPT_QW_MIN = 7
+    OPT_QW_STAGGER = 8
 
     def set_option(self, option: int, value: int) -> None:
         """Kernel-choice option (``hcr_index_set_option``); never changes results.
@@ -199,7 +200,8 @@ class VectorIndex:
         1 64-deep, 3 128-deep.
         ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel, 1 v4, 2 QW (0 heuristic).
         ``VectorIndex.OPT_QW_DM``: QW's stage LDS-DMA issue, -1 default, 0 at the barrier, 3 spread.
-        ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic)."""
+        ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic).
+        ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 1, the default / 0 / 1)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
 

@@ -71,8 +71,14 @@ def test_property_graph_store_and_context_retriever(tmp_path):
     kg4, sc4 = st2.vector_query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=10))
     assert [n.id for n in kg4] == [n.id for n in kg3]
     assert len(st2.get_triplets()) == len(st.get_triplets())
+    # any similarity_top_k (r05): 4096 > the live nodes -> every live node, ranked (deep path)
+    kg5, sc5 = st.vector_query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=4096))
+    live = np.array([f"e{i}" != kg[0].id for i in range(len(nodes))])
+    es5, ei5 = O.cosine_topk(q[None], E.astype(np.float64), int(live.sum()), rowmask=live)
+    assert [n.id for n in kg5] == [f"e{i}" for i in ei5[0]]
+    np.testing.assert_allclose(sc5, es5[0], atol=1e-12)
     with pytest.raises(ValueError):
-        st.vector_query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=4096))
+        st.vector_query(VectorStoreQuery(query_embedding=q.tolist(), similarity_top_k=-1))
 
 
 def test_vector_store_large_top_k_and_replace():

@@ -213,3 +213,34 @@ def test_qw_dma_modes_agree(hc, D):
                 st = ix.last_stats()
                 assert st["score_kernel"] == QW and st["uncertified_queries"] == 0, (dm, st)
                 _check(s[sub], i[sub], es, ei)
+
+
+@pytest.mark.parametrize("B", [200, 600])
+def test_qw_stagger_agrees(hc, B):
+    """HCR_OPT_QW_STAGGER (D = 384: waves 4-7 run each stage's test one stage late, two
+    accumulator sets) against the oracle and the plain form, one and three query blocks, an
+    odd stage count and a corpus tail, planted queries, a duplicate cluster (appends and
+    compactions in the late epilogue)."""
+    rng = np.random.default_rng(B + 21)
+    D, k = 384, 16
+    N = 64 * 777 + 29
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    E[1000:1400] = E[5] + 1e-3 * rng.standard_normal((400, D)).astype(np.float32)
+    Q, src = _planted(rng, E, B, with_src=True)
+    Q[:3] = E[5]
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        sub = np.r_[0:24, B - 16:B]
+        es, ei = O.cosine_topk(Q[sub], R, k)
+        outs = []
+        for stg in (0, 1):
+            ix.set_option(ix.OPT_QW_STAGGER, stg)
+            s, i = ix.search(Q, k)
+            st = ix.last_stats()
+            assert st["score_kernel"] == QW and st["uncertified_queries"] == 0, (stg, st)
+            _check(s[sub], i[sub], es, ei)
+            np.testing.assert_array_equal(i[3: B // 2, 0], src[3:])
+            outs.append((s, i))
+        np.testing.assert_array_equal(outs[0][1], outs[1][1])
+        np.testing.assert_array_equal(outs[0][0], outs[1][0])
