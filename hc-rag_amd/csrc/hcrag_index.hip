@@ -443,7 +443,7 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
       ix->opt_qw_dm = value;
       return HCR_OK;
     case HCR_OPT_QW_STAGGER:
-      if (value < -1 || value > 1) return set_err(HCR_EINVAL, "HCR_OPT_QW_STAGGER value %d not in [-1, 1]", value);
+      if (value < -1 || value > 2) return set_err(HCR_EINVAL, "HCR_OPT_QW_STAGGER value %d not in [-1, 2]", value);
       ix->opt_qw_stagger = value;
       return HCR_OK;
     case HCR_OPT_QW_MIN:

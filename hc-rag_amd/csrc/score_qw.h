@@ -119,7 +119,7 @@ __device__ __forceinline__ uint32_t qw_ord32(float f) {
 // epilogue, and wait ~2.4k cycles per stage at the barrier for waves 4-7, whose epilogue then
 // runs with the MFMA pipe idle.
 template <typename TM, int CAP, int KS, int SR_ = qw_sr(KS), int NST_ = QW_NST, bool MAXONLY = false,
-          bool SPREAD = false, bool STG = false>
+          bool SPREAD = false, int STG = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
                      const TM* __restrict__ qhat, int nqb, int P, int ntiles,
@@ -232,6 +232,45 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   bool need = false;
   uint64_t tkr[2] = {0ull, 0ull};
   float umx[2] = {0.f, 0.f};                         // MAXONLY: the current unit's maxima
+  // Candidate counts of the lane's two queries (qle, qle + 16), the same in the query's 4 lanes
+  // (l, l ^ 16, l ^ 32, l ^ 48).  A query belongs to one wave, so an append takes its slot from
+  // the wave's ballot -- the lanes below it with a key for the same query -- instead of an LDS
+  // counter round trip (r05: ~1.5k cycles per append under the fragment reads' LDS load).  The
+  // LDS counts are written only for a compaction and the final lists.
+  // (packed: query qle in the low half, qle + 16 in the high half -- one VGPR; the D = 768 loop
+  // has none to spare)
+  uint32_t cqp = 0u;
+  // the stage's appends: every score >= thr whose key beats the local k'-th key, per query n
+  auto append_stage = [&](const floatx4 (&acc)[RB][2], const bool (&hit)[2], const float (&thr)[2],
+                          uint32_t row0u, int lq, int le, int qle) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      if (!__any(hit[n])) continue;
+#pragma unroll
+      for (int m = 0; m < RB; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sc = acc[m][n][r];
+          const bool c = sc >= thr[n];
+          if (__builtin_amdgcn_ballot_w64(c)) {
+            const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
+            const bool a = c && key > tkr[n];
+            const uint64_t ba = __builtin_amdgcn_ballot_w64(a);
+            if (ba) {
+              // the 4 lanes of this lane's query (l & 15) + 16 j, j = 0..3, as a nibble
+              const uint64_t t = ba >> (le & 15);
+              const uint32_t nib = (uint32_t)(t & 1u) | (uint32_t)((t >> 15) & 2u) |
+                                   (uint32_t)((t >> 30) & 4u) | (uint32_t)((t >> 45) & 8u);
+              const uint32_t base = (cqp >> (16 * n)) & 0xFFFFu;
+              if (a) wbuf[(size_t)(qle + 16 * n) * CAP + base + __popc(nib & ((1u << lq) - 1u))] = key;
+              cqp += (uint32_t)__popc(nib) << (16 * n);
+            }
+          }
+        }
+      }
+    }
+    need = (cqp & 0xFFFFu) > (uint32_t)(CAP - SR) || (cqp >> 16) > (uint32_t)(CAP - SR);
+  };
 #ifdef HCR_QW_STAMPS
   uint64_t st_t0, st_t1, st_t2, st_t3, st_t4, st_acc[4] = {0, 0, 0, 0};
   const uint64_t st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
@@ -313,31 +352,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         float thr[2];
         thr[0] = unord32(max((uint32_t)(tkr[0] >> 32), tg[0]));
         thr[1] = unord32(max((uint32_t)(tkr[1] >> 32), tg[1]));
-        const uint32_t row0u = (uint32_t)row0;
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          if (!__any(hit[n])) continue;
-#pragma unroll
-          for (int m = 0; m < RB; ++m) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float sc = acc[m][n][r];
-              const bool c = sc >= thr[n];
-              if (__builtin_amdgcn_ballot_w64(c)) {
-                if (c) {
-                  const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
-                  if (key > tkr[n]) {
-                    const int ql = qle + 16 * n;
-                    const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-                    wbuf[(size_t)ql * CAP + pos] = key;
-                    need |= pos + 1 > CAP - SR;
-                  }
-                }
-              }
-            }
-          }
-        }
+        append_stage(acc, hit, thr, (uint32_t)row0, lq, le, qle);
         if (__any(need)) {
+          if (le < 16) { cnt[qle] = (int)(cqp & 0xFFFFu); cnt[qle + 16] = (int)(cqp >> 16); }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -349,6 +366,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
           need = false;
           tkr[0] = v3_lds_u64(tau_key + qle);
           tkr[1] = v3_lds_u64(tau_key + qle + 16);
+          cqp = v3_lds_u32(cnt + qle) | (v3_lds_u32(cnt + qle + 16) << 16);
         }
       }
     };
@@ -376,7 +394,12 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       mfma_stage(acc, st, nd, tg);
       if (!late) epilogue(acc, s, tg);
     };
-    floatx4 acc0[RB][2], acc1[RB][2];
+    // STG 1: two accumulator sets (the late waves' epilogue of stage s - 1 free to interleave with
+    // the MFMAs of stage s; 256 VGPRs, 2 spilled); STG 2: one set (228 VGPRs) -- the late waves
+    // test stage s - 1 before their MFMAs of stage s overwrite it.  (D = 768 has no room for
+    // either: its plain loop already holds 256 VGPRs; built, it went to 704 B of scratch.)
+    floatx4 acc0[RB][2], acc1s[RB][2];
+    floatx4 (&acc1)[RB][2] = STG == 1 ? acc1s : acc0;
     uint32_t tg0[2] = {0u, 0u}, tg1[2] = {0u, 0u};
     int s = 0;
     for (; s + 1 < nsteps; s += 2) {
@@ -526,33 +549,11 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
       float thr[2];
       thr[0] = unord32(max((uint32_t)(tkr[0] >> 32), tg2[0]));
       thr[1] = unord32(max((uint32_t)(tkr[1] >> 32), tg2[1]));
-      const uint32_t row0u = (uint32_t)row0;
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        if (!__any(hit[n])) continue;
-#pragma unroll
-        for (int m = 0; m < RB; ++m) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float sc = acc[m][n][r];
-            const bool c = sc >= thr[n];
-            if (__builtin_amdgcn_ballot_w64(c)) {
-              if (c) {
-                const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
-                if (key > tkr[n]) {
-                  const int ql = qle + 16 * n;
-                  const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-                  wbuf[(size_t)ql * CAP + pos] = key;
-                  need |= pos + 1 > CAP - SR;
-                }
-              }
-            }
-          }
-        }
-      }
+      append_stage(acc, hit, thr, (uint32_t)row0, lq, le, qle);
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drains this wave's stores and, in order, its ring pieces)
       if (__any(need)) {
+        if (le < 16) { cnt[qle] = (int)(cqp & 0xFFFFu); cnt[qle + 16] = (int)(cqp >> 16); }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -564,6 +565,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         need = false;
         tkr[0] = v3_lds_u64(tau_key + qle);
         tkr[1] = v3_lds_u64(tau_key + qle + 16);
+        cqp = v3_lds_u32(cnt + qle) | (v3_lds_u32(cnt + qle + 16) << 16);
       }
     }
 #ifdef HCR_QW_STAMPS
@@ -587,6 +589,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (MAXONLY) return;
+  if (lane < 16) { cnt[wq0 + lane] = (int)(cqp & 0xFFFFu); cnt[wq0 + lane + 16] = (int)(cqp >> 16); }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 32, kp, lane, partials, pcnt, P, p);
 }

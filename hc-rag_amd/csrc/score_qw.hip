@@ -29,7 +29,7 @@ bool qw_spread(int dm, int nqb) {
   return m == 3;
 }
 
-template <typename TM, int CAP, int KS, int SR, int NST, bool SPREAD, bool STG = false>
+template <typename TM, int CAP, int KS, int SR, int NST, bool SPREAD, int STG = 0>
 void launch_dense(const QsArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((score_topk_qw_kernel<TM, CAP, KS, SR, NST, false, SPREAD, STG>), dim3(a.nqb * a.P),
                      dim3(V3_NT), 0, st, static_cast<const TM*>(a.rows), a.ld, a.n_rows,
@@ -48,13 +48,20 @@ void launch_t(const QsArgs& a, hipStream_t st) {
     }
   }
   const bool spread = qw_spread(a.dm, a.nqb);
-  // STG: D = 384 only (two accumulator sets fit); on by default -- r05k interleaved A/B on one
-  // box, score phase: 1M x 384 B = 256 0.2277 -> 0.2257 ms, B = 1024 0.7654 -> 0.7455 ms
-  // (profiles/r05/r05k/)
+  // STG: D = 384 only (QW's plain D = 768 loop already holds 256 VGPRs).  On by default with one
+  // accumulator set -- interleaved A/B on one box, score phase (profiles/r05/r05k, r05l):
+  // 1M x 384 B = 256 0.2452 (off) / 0.2400 (two sets) / 0.2370 ms (one set); B = 1024 0.7778 /
+  // 0.7493 / 0.7454 ms
   if constexpr (KS == 12) {
-    if (a.stagger != 0) {
-      if (spread) launch_dense<TM, CAP, KS, SR, NST, true, true>(a, st);
-      else launch_dense<TM, CAP, KS, SR, NST, false, true>(a, st);
+    const int stg = a.stagger < 0 ? 2 : a.stagger;
+    if (stg == 2) {
+      if (spread) launch_dense<TM, CAP, KS, SR, NST, true, 2>(a, st);
+      else launch_dense<TM, CAP, KS, SR, NST, false, 2>(a, st);
+      return;
+    }
+    if (stg == 1) {
+      if (spread) launch_dense<TM, CAP, KS, SR, NST, true, 1>(a, st);
+      else launch_dense<TM, CAP, KS, SR, NST, false, 1>(a, st);
       return;
     }
   }

@@ -222,6 +222,12 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   const uint32_t lds0 = lds_addr(lds);
 
   bool need = false;
+  // candidate counts of the lane's QB queries, the same in a query's 4 lanes (a query belongs to
+  // one wave: appends take their slots from the wave's ballot); LDS cnt[] is written for a
+  // compaction and the final lists
+  int cq[QB];
+#pragma unroll
+  for (int n = 0; n < QB; ++n) cq[n] = 0;
   uint64_t tkr[QB];
 #pragma unroll
   for (int n = 0; n < QB; ++n) tkr[n] = 0ull;
@@ -374,22 +380,28 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
             const float sc = acc[m][n][r];
             const bool c = sc >= thr[n];
             if (__builtin_amdgcn_ballot_w64(c)) {
-              if (c) {
-                const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
-                if (key > tkr[n]) {
-                  const int ql = qle + 16 * n;
-                  const int pos = v3_lds_add_rtn(&cnt[ql], 1);
-                  wbuf[(size_t)ql * CAP + pos] = key;
-                  need |= pos + 1 > CAP - SR;
-                }
+              // the slot from the wave's ballot (QW's r05 form: no LDS counter round trip)
+              const uint64_t key = make_key(sc, row0u + (uint32_t)(m * 16 + lq * 4 + r));
+              const bool a = c && key > tkr[n];
+              const uint64_t ba = __builtin_amdgcn_ballot_w64(a);
+              if (ba) {
+                const uint64_t t = ba >> (le & 15);
+                const uint32_t nib = (uint32_t)(t & 1u) | (uint32_t)((t >> 15) & 2u) |
+                                     (uint32_t)((t >> 30) & 4u) | (uint32_t)((t >> 45) & 8u);
+                if (a) wbuf[(size_t)(qle + 16 * n) * CAP + cq[n] + __popc(nib & ((1u << lq) - 1u))] = key;
+                cq[n] += __popc(nib);
               }
             }
           }
         }
+        need |= cq[n] > CAP - SR;
       }
       // a query whose buffer cannot take another tile's appends is compacted to its best k'
       // (rare: drains this wave's stores and, in order, its ring pieces)
       if (__any(need)) {
+#pragma unroll
+        for (int n = 0; n < QB; ++n)
+          if (le < 16) cnt[qle + 16 * n] = cq[n];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 #pragma unroll 1
@@ -400,7 +412,10 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
         }
         need = false;
 #pragma unroll
-        for (int n = 0; n < QB; ++n) tkr[n] = v3_lds_u64(tau_key + qle + 16 * n);
+        for (int n = 0; n < QB; ++n) {
+          tkr[n] = v3_lds_u64(tau_key + qle + 16 * n);
+          cq[n] = (int)v3_lds_u32(cnt + qle + 16 * n);
+        }
       }
     }
 #ifdef HCR_QW1_STAMPS
@@ -419,6 +434,9 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int n = 0; n < QB; ++n)
+    if (lane < 16) cnt[wq0 + lane + 16 * n] = cq[n];
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + QPW, kp, lane, partials, pcnt, P, p);
 }

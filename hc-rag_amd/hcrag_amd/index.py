@@ -201,7 +201,7 @@ class VectorIndex:
         ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel, 1 v4, 2 QW (0 heuristic).
         ``VectorIndex.OPT_QW_DM``: QW's stage LDS-DMA issue, -1 default, 0 at the barrier, 3 spread.
         ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic).
-        ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 1, the default / 0 / 1)."""
+        ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 2, the default; 1 / 2 = two / one accumulator sets; 0 = off)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
 

@@ -174,8 +174,9 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                stage barrier, 3 = spread over the MFMA groups.  (1, 2, 4, 5: measured in r05,
  *                removed.)
  *   HCR_OPT_QW_MIN: the smallest batch the QW kernel takes (0 = the heuristic: 129).
- *   HCR_OPT_QW_STAGGER: QW at D = 384 -- 1 = waves 4-7 run each stage's top-k' test one stage
- *                late (beside the other waves' MFMAs), 0 = off, -1 = the default (1). */
+ *   HCR_OPT_QW_STAGGER: QW at D = 384 -- waves 4-7 run each stage's top-k' test one stage
+ *                late (beside the other waves' MFMAs): 1 = with two accumulator sets, 2 = with
+ *                one, 0 = off, -1 = the default (2). */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,
                HCR_OPT_PREPASS = 5, HCR_OPT_QW_DM = 6, HCR_OPT_QW_MIN = 7,
                HCR_OPT_QW_STAGGER = 8 } hcr_index_option;

@@ -234,7 +234,7 @@ def test_qw_stagger_agrees(hc, B):
         sub = np.r_[0:24, B - 16:B]
         es, ei = O.cosine_topk(Q[sub], R, k)
         outs = []
-        for stg in (0, 1):
+        for stg in (0, 1, 2):
             ix.set_option(ix.OPT_QW_STAGGER, stg)
             s, i = ix.search(Q, k)
             st = ix.last_stats()
@@ -242,5 +242,6 @@ def test_qw_stagger_agrees(hc, B):
             _check(s[sub], i[sub], es, ei)
             np.testing.assert_array_equal(i[3: B // 2, 0], src[3:])
             outs.append((s, i))
-        np.testing.assert_array_equal(outs[0][1], outs[1][1])
+        for o in outs[1:]:
+            np.testing.assert_array_equal(outs[0][1], o[1])
         np.testing.assert_array_equal(outs[0][0], outs[1][0])
