@@ -878,6 +878,12 @@ seed_select_kernel(const float* __restrict__ umax, int U, int nqpad, int nq, int
   }
 }
 
+#ifdef HCR_FINISH_STAMPS
+extern "C" int hcr_debug_finish_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hcr::hcr_fin_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // HCRAG_TEST_PLANT_BAD_KEY: slot 0 of query 0's first list := the key (score 2.0, row)
 __global__ void plant_key_kernel(uint64_t* __restrict__ list, int* __restrict__ cnt, uint32_t row) {
   if (threadIdx.x == 0) {

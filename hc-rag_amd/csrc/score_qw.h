@@ -142,6 +142,9 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef HCR_QW_STAMPS
+  const uint64_t st_e0 = __builtin_amdgcn_s_memrealtime();   // kernel entry (100 MHz ticks)
+#endif
 
   const int nwg = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -579,19 +582,26 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
 #endif
   }
 #ifdef HCR_QW_STAMPS
-  if (!MAXONLY && lane == 0 && b < 4096) {
-    unsigned long long* o = hcr_qw_stamps + ((size_t)b * 8 + wave) * 8;
-    o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = st_acc[3]; o[4] = nsteps;
-    o[5] = __builtin_amdgcn_s_memtime() - st_c0;          // shader cycles over the loop ...
-    o[6] = __builtin_amdgcn_s_memrealtime() - st_r0;      // ... and 100 MHz ticks: the clock
-  }
+  const uint64_t st_c1 = __builtin_amdgcn_s_memtime(), st_r1 = __builtin_amdgcn_s_memrealtime();
 #endif
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (MAXONLY) return;
   if (lane < 16) { cnt[wq0 + lane] = (int)(cqp & 0xFFFFu); cnt[wq0 + lane + 16] = (int)(cqp >> 16); }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, wq0 + 32, kp, lane, partials, pcnt, P, p);
+  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 32, kp, lane, partials, pcnt, P, p);
+#ifdef HCR_QW_STAMPS
+  if (lane == 0 && b < 4096) {
+    // o[4]: stages | prologue ticks << 24 | final-lists ticks << 44; o[7]: entry (absolute)
+    const uint64_t st_r2 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* o = hcr_qw_stamps + ((size_t)b * 8 + wave) * 8;
+    o[0] = st_acc[0]; o[1] = st_acc[1]; o[2] = st_acc[2]; o[3] = st_acc[3];
+    o[4] = (uint64_t)nsteps | ((st_r0 - st_e0) << 24) | ((st_r2 - st_r1) << 44);
+    o[5] = st_c1 - st_c0;                                  // shader cycles over the loop ...
+    o[6] = st_r1 - st_r0;                                  // ... and 100 MHz ticks: the clock
+    o[7] = st_e0;
+  }
+#endif
 }
 
 }  // namespace hcr

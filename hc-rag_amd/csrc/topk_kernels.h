@@ -267,6 +267,84 @@ __device__ __forceinline__ void final_lists(uint64_t* __restrict__ wbuf, int* cn
   }
 }
 
+// Final lists of a wave that owns the consecutive queries ql0 .. ql0 + nqw - 1 (nqw <= 64: QW,
+// QW1, QS), same output as final_lists.  final_lists walks the queries one after another, one
+// dependent global load per query (the global bound, the buffer): ~18 us at the end of every
+// configs[1] launch and ~25 us at the W = 8 rank shape (r05p stamps), 9 % of the former's dense
+// pass.  Here lane l < nqw reads query l's count and bound at once, the candidates of all queries
+// whose buffer holds <= kp keys are laid end to end (a wave prefix sum of the counts) and read
+// 4 x 64 at a time -- one memory latency per 256 candidates, not per query -- and each kept key
+// takes its slot in its query's list from the ballot.  A query with more than kp candidates (a
+// full buffer: rare) goes through final_lists' wave sort.  (Not inlined: inlined, the score
+// kernels' register allocation around their main loops changed and spilled.)
+__device__ __forceinline__ uint64_t fl_mask_lt(int x) { return x >= 64 ? ~0ull : x <= 0 ? 0ull : (1ull << x) - 1ull; }
+
+template <int CAP>
+__device__ __attribute__((noinline)) void final_lists_wave(uint64_t* __restrict__ wbuf, int* cnt, uint64_t* tau_key,
+                                                 uint32_t* tau_g, int qbase, int ql0, int nqw, int kp,
+                                                 int lane, uint64_t* __restrict__ partials,
+                                                 int* __restrict__ pcnt, int P, int p) {
+  const bool qlive = lane < nqw;
+  const int my_c = qlive ? cnt[ql0 + lane] : 0;
+  const uint32_t my_tg =
+      qlive ? __hip_atomic_load(tau_g + qbase + ql0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  const bool big = my_c > kp;
+  const int fc = big ? 0 : my_c;                   // candidates this query puts in the gather
+  int incl = fc;                                    // inclusive prefix sum of fc over the lanes
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  const int excl = incl - fc;
+  const int T = __shfl(incl, 63, 64);
+  int nk = 0;                                       // keys kept so far (lane l: query l)
+  constexpr int R = 4;
+  for (int base = 0; base < T; base += 64 * R) {
+    int qv[R];
+    uint64_t kv[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int idx = base + u * 64 + lane;
+      // the query of candidate idx: the last lane with excl <= idx (a query with fc = 0 shares
+      // its excl with the next one, so the last such lane owns idx < T)
+      int lo = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int cand = lo + step;
+        const int e = __shfl(excl, cand < 64 ? cand : 63, 64);
+        if (cand < nqw && e <= idx) lo = cand;
+      }
+      qv[u] = lo;
+      const int off = idx - __shfl(excl, lo, 64);
+      kv[u] = idx < T ? wbuf[(size_t)(ql0 + lo) * CAP + off] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int b0 = base + u * 64;
+      if (b0 >= T) break;
+      const int q = qv[u];
+      const uint64_t key = kv[u];
+      const bool keep = key != 0ull && (uint32_t)(key >> 32) >= (uint32_t)__shfl((int)my_tg, q, 64);
+      const uint64_t m = __ballot(keep);
+      // this chunk's lanes of query q are [excl_q - b0, ...): the kept ones below this lane
+      const int s_q = __shfl(excl, q, 64) - b0;
+      const int pos = __shfl(nk, q, 64) + __popcll(m & fl_mask_lt(lane) & ~fl_mask_lt(s_q));
+      if (keep) partials[((size_t)(qbase + ql0 + q) * P + p) * kp + pos] = key;
+      // every query lane: its kept keys of this chunk
+      nk += __popcll(m & fl_mask_lt(excl + fc - b0) & ~fl_mask_lt(excl - b0));
+    }
+  }
+  if (qlive && !big) pcnt[(size_t)(qbase + ql0 + lane) * P + p] = nk;
+  // queries whose buffer holds more than kp keys: final_lists' path, one at a time
+  uint64_t bigm = __ballot(big);
+  while (bigm) {
+    const int l = __builtin_ctzll(bigm);
+    bigm &= bigm - 1;
+    final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, ql0 + l, 1, ql0 + l + 1, kp, lane, partials, pcnt, P, p);
+  }
+}
+
 template <int CAP>
 __device__ __attribute__((noinline)) void compact_query(uint64_t* __restrict__ qbuf, int* cnt_q,
                                                       uint64_t* tau_key_q, uint32_t* tau_g_q,
@@ -637,6 +715,18 @@ __device__ __forceinline__ void acc8_f64(double& acc, const TQ* __restrict__ q, 
 // -------------------------------------------------------------------------------------
 // K4: exact fp64 rescoring + certificate + final top-k.
 // -------------------------------------------------------------------------------------
+#ifdef HCR_FINISH_STAMPS
+// diagnostic build (Makefile stamps_fin): per block (query), s_memrealtime at the phase
+// boundaries of finish_kernel / rescore_kernel: [q][8] (tools/finish_stamps.py)
+__device__ unsigned long long hcr_fin_stamps[4096 * 8];
+#define HCR_FIN_STAMP(i)                                                                       \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                                  \
+      hcr_fin_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
+#else
+#define HCR_FIN_STAMP(i) do {} while (0)
+#endif
 // The body of K4 for one query (block): `keys` (LDS) holds its merged top-kp coarse keys,
 // sorted descending and zero padded, `qd` (LDS) the fp32 query widened to fp64; hi / lo / nrm
 // are kp-slot LDS arrays.  Writes the query's top-k, its certificate flag and s_k.
@@ -665,6 +755,7 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
   }
   if (threadIdx.x == 0) *s_nvalid = 0;
   __syncthreads();
+  HCR_FIN_STAMP(2);
   const double qn = qnorm[q];
   // RU candidates per wave at a time, their 16-byte row loads in flight together; per
   // candidate the summation order is acc8_f64's (K6's).  RU = 8 (r03): ~100 VGPRs, so 4 blocks
@@ -706,7 +797,9 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
     }
   }
   __syncthreads();
+  HCR_FIN_STAMP(3);
   block_sort_desc_pair_fast(hi, lo, kp);
+  HCR_FIN_STAMP(4);
   const int nvalid = *s_nvalid;
   if (threadIdx.x == 0) {
     // Every row outside the candidates has coarse score <= B: the k'-th candidate's coarse
@@ -736,6 +829,7 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
     out_s[(size_t)q * k + t] = s;
     out_i[(size_t)q * k + t] = id;
   }
+  HCR_FIN_STAMP(5);
 }
 
 #define HCR_RESCORE_PARAMS                                                                          \
@@ -786,9 +880,11 @@ finish_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, i
   double* nrm = reinterpret_cast<double*>(lo + kp);
   int* s_nvalid = reinterpret_cast<int*>(nrm + kp);
   const int q = blockIdx.x;
+  HCR_FIN_STAMP(0);
   const float* src = q32 + (int64_t)q * dim;
   for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];   // (under the merge)
   merge_block_lds(lists, cnt, P, 0, P, kp, q, sm_keys, s_off, s_hist, s_misc);
+  HCR_FIN_STAMP(1);
   rescore_block<TS>(sm_keys, qd, hi, lo, nrm, s_nvalid, HCR_RESCORE_ARGS);
 }
 

@@ -38,7 +38,12 @@ fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 n = 4096 * 8 * 8
 buf = (ctypes.c_ulonglong * n)()
 assert fn(buf, n) == 0
-a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8, 8).astype(np.float64)
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8, 8)
+a = raw.astype(np.float64)
+o4 = raw[:, :, 4]
+a[:, :, 4] = (o4 & np.uint64(0xFFFFFF)).astype(np.float64)          # stages
+pro = ((o4 >> np.uint64(24)) & np.uint64(0xFFFFF)).astype(np.float64) / 100.0   # us
+fin = (o4 >> np.uint64(44)).astype(np.float64) / 100.0
 parts = ["wait+barrier", "dma+bounds", "mfma groups", "epilogue"]
 live0 = a[:, :, 6] > 0
 ghz = np.median(a[:, :, 5][live0] / a[:, :, 6][live0]) * 0.1 if live0.any() else 0.0
@@ -55,3 +60,17 @@ for name, sel in (("all waves", slice(0, 8)), ("waves 0-3", slice(0, 4)), ("wave
         x = sub[:, :, i][live] / stages
         print(f"  {nm:14s} {x.mean():8.0f} cycles/stage (p10 {np.percentile(x, 10):7.0f}, "
               f"p90 {np.percentile(x, 90):7.0f})  share {sub[:, :, i][live].sum() / tot:.3f}")
+# the launch's time line per wave (100 MHz ticks -> us): entry skew, prologue (query fragments,
+# ring primed), the stage loop, the final lists
+live = a[:, :, 4] > 0
+if live.any():
+    e0 = raw[:, :, 7][live].astype(np.float64) / 100.0
+    loop = a[:, :, 6][live] / 100.0
+    p_, f_ = pro[live], fin[live]
+    t0 = e0.min()
+    end = e0 - t0 + p_ + loop + f_
+    print(f"time line (us, median / p90 / max over waves): entry skew {np.median(e0 - t0):.1f} / "
+          f"{np.percentile(e0 - t0, 90):.1f} / {(e0 - t0).max():.1f}; prologue {np.median(p_):.1f} / "
+          f"{np.percentile(p_, 90):.1f} / {p_.max():.1f}; loop {np.median(loop):.1f} / "
+          f"{np.percentile(loop, 90):.1f} / {loop.max():.1f}; final lists {np.median(f_):.1f} / "
+          f"{np.percentile(f_, 90):.1f} / {f_.max():.1f}; last wave ends at {end.max():.1f}")
