@@ -557,7 +557,7 @@ score_topk_qs_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
     if (lane < 16) v3_lds_store_u32(&cnt[qlane + 16 * n], (uint32_t)cntr[n]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 16 * NQ, kp, lane, partials, pcnt, P, p);
+  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, 16 * NQ, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

@@ -589,7 +589,7 @@ score_topk_qw_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   if constexpr (MAXONLY) return;
   if (lane < 16) { cnt[wq0 + lane] = (int)(cqp & 0xFFFFu); cnt[wq0 + lane + 16] = (int)(cqp >> 16); }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 32, kp, lane, partials, pcnt, P, p);
+  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, 32, kp, lane, partials, pcnt, P, p);
 #ifdef HCR_QW_STAMPS
   if (lane == 0 && b < 4096) {
     // o[4]: stages | prologue ticks << 24 | final-lists ticks << 44; o[7]: entry (absolute)

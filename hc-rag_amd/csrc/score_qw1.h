@@ -438,7 +438,7 @@ score_topk_qw1_kernel(const TM* __restrict__ rows, int ld, int64_t n_rows,
   for (int n = 0; n < QB; ++n)
     if (lane < 16) cnt[wq0 + lane + 16 * n] = cq[n];
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, QPW, kp, lane, partials, pcnt, P, p);
+  final_lists_wave<CAP>(wbuf, cnt, tau_key, tau_g, qbase, wq0, 1, QPW, kp, lane, partials, pcnt, P, p);
 }
 
 }  // namespace hcr

@@ -267,8 +267,9 @@ __device__ __forceinline__ void final_lists(uint64_t* __restrict__ wbuf, int* cn
   }
 }
 
-// Final lists of a wave that owns the consecutive queries ql0 .. ql0 + nqw - 1 (nqw <= 64: QW,
-// QW1, QS), same output as final_lists.  final_lists walks the queries one after another, one
+// Final lists of a wave's queries ql0 + i qstep, i < nqw <= 64 (QW, QW1, QS: consecutive, one
+// workgroup of 8 waves per CU), same output as final_lists.  (v3 / v4 / K2 keep final_lists: this
+// call's registers -- 248 VGPRs at CAP = 1024 -- would cut their occupancy.)  final_lists walks the queries one after another, one
 // dependent global load per query (the global bound, the buffer): ~18 us at the end of every
 // configs[1] launch and ~25 us at the W = 8 rank shape (r05p stamps), 9 % of the former's dense
 // pass.  Here lane l < nqw reads query l's count and bound at once, the candidates of all queries
@@ -281,13 +282,14 @@ __device__ __forceinline__ uint64_t fl_mask_lt(int x) { return x >= 64 ? ~0ull :
 
 template <int CAP>
 __device__ __attribute__((noinline)) void final_lists_wave(uint64_t* __restrict__ wbuf, int* cnt, uint64_t* tau_key,
-                                                 uint32_t* tau_g, int qbase, int ql0, int nqw, int kp,
+                                                 uint32_t* tau_g, int qbase, int ql0, int qstep, int nqw, int kp,
                                                  int lane, uint64_t* __restrict__ partials,
                                                  int* __restrict__ pcnt, int P, int p) {
   const bool qlive = lane < nqw;
-  const int my_c = qlive ? cnt[ql0 + lane] : 0;
+  const int my_ql = ql0 + lane * qstep;
+  const int my_c = qlive ? cnt[my_ql] : 0;
   const uint32_t my_tg =
-      qlive ? __hip_atomic_load(tau_g + qbase + ql0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      qlive ? __hip_atomic_load(tau_g + qbase + my_ql, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   const bool big = my_c > kp;
   const int fc = big ? 0 : my_c;                   // candidates this query puts in the gather
   int incl = fc;                                    // inclusive prefix sum of fc over the lanes
@@ -317,7 +319,7 @@ __device__ __attribute__((noinline)) void final_lists_wave(uint64_t* __restrict_
       }
       qv[u] = lo;
       const int off = idx - __shfl(excl, lo, 64);
-      kv[u] = idx < T ? wbuf[(size_t)(ql0 + lo) * CAP + off] : 0ull;
+      kv[u] = idx < T ? wbuf[(size_t)(ql0 + lo * qstep) * CAP + off] : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -330,18 +332,18 @@ __device__ __attribute__((noinline)) void final_lists_wave(uint64_t* __restrict_
       // this chunk's lanes of query q are [excl_q - b0, ...): the kept ones below this lane
       const int s_q = __shfl(excl, q, 64) - b0;
       const int pos = __shfl(nk, q, 64) + __popcll(m & fl_mask_lt(lane) & ~fl_mask_lt(s_q));
-      if (keep) partials[((size_t)(qbase + ql0 + q) * P + p) * kp + pos] = key;
+      if (keep) partials[((size_t)(qbase + ql0 + q * qstep) * P + p) * kp + pos] = key;
       // every query lane: its kept keys of this chunk
       nk += __popcll(m & fl_mask_lt(excl + fc - b0) & ~fl_mask_lt(excl - b0));
     }
   }
-  if (qlive && !big) pcnt[(size_t)(qbase + ql0 + lane) * P + p] = nk;
+  if (qlive && !big) pcnt[(size_t)(qbase + my_ql) * P + p] = nk;
   // queries whose buffer holds more than kp keys: final_lists' path, one at a time
   uint64_t bigm = __ballot(big);
   while (bigm) {
     const int l = __builtin_ctzll(bigm);
     bigm &= bigm - 1;
-    final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, ql0 + l, 1, ql0 + l + 1, kp, lane, partials, pcnt, P, p);
+    final_lists<CAP>(wbuf, cnt, tau_key, tau_g, qbase, ql0 + l * qstep, 1, ql0 + l * qstep + 1, kp, lane, partials, pcnt, P, p);
   }
 }
 
