@@ -732,7 +732,7 @@ __device__ unsigned long long hcr_fin_stamps[4096 * 8];
 // The body of K4 for one query (block): `keys` (LDS) holds its merged top-kp coarse keys,
 // sorted descending and zero padded, `qd` (LDS) the fp32 query widened to fp64; hi / lo / nrm
 // are kp-slot LDS arrays.  Writes the query's top-k, its certificate flag and s_k.
-template <typename TS>
+template <typename TS, int RU = 8>
 __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, uint64_t* hi,
                                               uint64_t* lo, double* nrm, int* s_nvalid, int q, int kp,
                                               int dim, const double* __restrict__ qnorm,
@@ -760,10 +760,12 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
   HCR_FIN_STAMP(2);
   const double qn = qnorm[q];
   // RU candidates per wave at a time, their 16-byte row loads in flight together; per
-  // candidate the summation order is acc8_f64's (K6's).  RU = 8 (r03): ~100 VGPRs, so 4 blocks
-  // per CU are resident and a 1024-query batch is one round of blocks (RU = 16: 183 VGPRs, 2
-  // blocks per CU, two rounds of the block's dependent key -> row -> sort chain)
-  constexpr int RU = 8;
+  // candidate the summation order is acc8_f64's (K6's).  rescore_kernel: RU = 8 (r03): ~100
+  // VGPRs, so 4 blocks per CU are resident and a 1024-query batch is one round of blocks (RU =
+  // 16: 183 VGPRs, 2 blocks per CU, two rounds of the block's dependent key -> row -> sort chain).
+  // finish_kernel (<= 512 queries, at most 2 blocks per CU anyway): RU = 16, k' = 64 in one round
+  // of row gathers instead of two (r05r stamps: the fp64 dots were 13.4 of its 25 us at
+  // configs[1], two dependent HBM gathers)
   for (int c0 = wave * RU; c0 < kp; c0 += 4 * RU) {
     uint64_t kk[RU];
     const TS* e[RU];
@@ -781,22 +783,31 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
 #pragma unroll
       for (int u = 0; u < RU; ++u) acc8_f64(acc[u], qd, d0, dim, x[u]);
     }
+    // the RU wave sums side by side (wave_sum_f64's pairing and order, level by level: the same
+    // bits; one after another, each shuffle waited for the last -- r05r stamps: 13 of the finish
+    // kernel's 25 us at configs[1]), then lane u < RU finishes candidate c0 + u
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int c = c0 + u;
-      if (c >= kp) break;
-      const double a = wave_sum_f64(acc[u]);
-      if (lane == 0) {
-        if (kk[u] == 0ull) {
-          hi[c] = 0ull; lo[c] = 0ull;
-        } else {
-          const uint32_t row = key_row(kk[u]);
-          hi[c] = ord64(a / (qn * nrm[c]));
-          lo[c] = (uint64_t)(0xFFFFFFFFu - row);
-          atomicAdd(s_nvalid, 1);
-        }
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+      for (int u = 0; u < RU; ++u)
+        acc[u] += __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(acc[u]), m));
+    double a = 0.0;
+    uint64_t ku = 0ull;
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+      if (lane == u) { a = acc[u]; ku = kk[u]; }
+    const int c = c0 + lane;
+    const bool mine = lane < RU && c < kp;
+    if (mine) {
+      if (ku == 0ull) {
+        hi[c] = 0ull; lo[c] = 0ull;
+      } else {
+        hi[c] = ord64(a / (qn * nrm[c]));
+        lo[c] = (uint64_t)(0xFFFFFFFFu - key_row(ku));
       }
     }
+    const int nv = __popcll(__ballot(mine && ku != 0ull));
+    if (lane == 0 && nv) atomicAdd(s_nvalid, nv);
   }
   __syncthreads();
   HCR_FIN_STAMP(3);
@@ -887,7 +898,7 @@ finish_kernel(const uint64_t* __restrict__ lists, const int* __restrict__ cnt, i
   for (int d = threadIdx.x; d < dim; d += blockDim.x) qd[d] = (double)src[d];   // (under the merge)
   merge_block_lds(lists, cnt, P, 0, P, kp, q, sm_keys, s_off, s_hist, s_misc);
   HCR_FIN_STAMP(1);
-  rescore_block<TS>(sm_keys, qd, hi, lo, nrm, s_nvalid, HCR_RESCORE_ARGS);
+  rescore_block<TS, 16>(sm_keys, qd, hi, lo, nrm, s_nvalid, HCR_RESCORE_ARGS);
 }
 
 // -------------------------------------------------------------------------------------
