@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--batch", type=int, default=0,
                    help="queries per GPU per step (weak scaling; overrides --global-batch)")
     p.add_argument("--k", type=int, default=32)
+    p.add_argument("--global-seed", default="on", choices=["on", "off"],
+                   help="N > 1: seed every rank's dense pass from the all-gathered sample of the "
+                        "whole corpus (DESIGN.md §6); off: each rank seeds from its own shard")
     p.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     p.add_argument("--cpu-rows", type=int, default=1_000_000)
     p.add_argument("--cpu-queries", type=int, default=1024)
@@ -822,8 +825,12 @@ def main():
         return torch.stack(out).to(dev)
 
     Q, src = make_queries(rows_fn, B, D, dev, rank, nloc, r0)
-    from hcrag_amd.distributed import ShardedSearch, hip_local_search, hip_merge
-    searcher = ShardedSearch(hip_local_search(ix, k), hip_merge(k), k)
+    from hcrag_amd.distributed import ShardedSearch, hip_local_search, hip_merge, hip_global_seed
+    gs = hip_global_seed(ix, k, world, (N + 255) // 256) if (world > 1 and a.global_seed == "on"
+                                                              and k <= 256) else (None, None)
+    searcher = ShardedSearch(hip_local_search(ix, k), hip_merge(k), k, local_sample=gs[0],
+                             local_seeded=gs[1], n_local=nloc)
+    gs_reruns = []
 
     def step():
         return searcher.search(Q)[1]
@@ -840,6 +847,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         res = step()
+        gs_reruns.append(searcher.last_global_seed)
         st = ix.last_stats()
         kern_ms += st["score_kernel_ms"]
         launches += st["score_launches"]
@@ -960,7 +968,8 @@ def main():
                     "queries 50% planted (corpus row + noise) / 50% random, fp32, HBM-resident",
             "config": {"workload": workload_name(N, D, a.dtype, nq, k, world),
                        "rows": N, "dim": D, "batch_per_gpu": B, "global_batch": nq, "k": k,
-                       "parallelism": f"rowshard{world}" + ("+rccl_allgather_alltoall" if world > 1 else "")},
+                       "parallelism": f"rowshard{world}" + ("+rccl_allgather_alltoall" if world > 1 else ""),
+                       "global_seed": gs[0] is not None},
             "roofline": roof,
             "cpu_baseline": cpu,
             "encoder": enc_res,
@@ -976,7 +985,11 @@ def main():
                       "mfma_frac": round(flops / (avg_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
                       "hbm_frac_kernel": round(bytes_alg / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "pipeline_ms_per_step": round(elapsed / a.steps * 1e3, 3),
-                      "batch_sweep": sweep, "large_k": large_k},
+                      "batch_sweep": sweep, "large_k": large_k,
+                      "global_seed_reruns": (None if gs[0] is None else
+                                             sum(x for x in gs_reruns if x is not None)),
+                      "global_seed_plain_steps": (None if gs[0] is None else
+                                                  sum(1 for x in gs_reruns if x is None))},
         }
     ix.close()
     if rank == 0 and world == 1 and not a.no_configs4:

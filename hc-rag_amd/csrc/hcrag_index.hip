@@ -40,6 +40,16 @@ extern "C" int hcr_device_count(void) {
 // index object
 // ---------------------------------------------------------------------------------------
 struct hcr_index {
+  // global seed across shards (hcr_search_sample_device / hcr_search_seeded_device), set for one
+  // call: the sampling pass only (report the unit maxima), or the dense pass seeded from every
+  // shard's maxima with the per-query bound of the rows left out
+  bool gs_sample_only = false;
+  int gs_sample_units = 0, gs_sample_nqpad = 0;
+  int64_t gs_sample_rows = 0;
+  const float* gs_umax = nullptr;
+  int gs_units = 0;
+  double gs_frac = 0.0;
+  double* gs_bound = nullptr;
   int device = 0;
   int dim = 0;
   int ld = 0;           // row stride in elements (dim rounded up to 64, zero padded)
@@ -764,7 +774,7 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
-                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound);
 }
 
 // Merge of the last <= G lists + rescore in one launch (finish_kernel); false when its LDS
@@ -785,7 +795,7 @@ static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, i
                      ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
-                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr);
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound);
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -884,6 +894,11 @@ extern "C" int hcr_debug_finish_stamps(unsigned long long* host, int n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(hcr::hcr_fin_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
 }
 #endif
+
+__global__ void fill_f64(double* __restrict__ p, int64_t n, double v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
 
 // HCRAG_TEST_PLANT_BAD_KEY: slot 0 of query 0's first list := the key (score 2.0, row)
 __global__ void plant_key_kernel(uint64_t* __restrict__ list, int* __restrict__ cnt, uint32_t row) {
@@ -1062,7 +1077,24 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     // tau_g exactly; the dense pass then appends only rows that can still be in the top-k'.
     const TestHooks& th = hooks();
     const int min_tiles = th.prepass_min_tiles ? th.prepass_min_tiles : kPrepassMinTilesPerWg;
-    if (!th.no_prepass && ntiles >= (int64_t)P * min_tiles) {
+    if (ix->gs_umax) {
+      // global seed: the j-th largest of every shard's unit maxima ([U][nq], gathered by the
+      // caller), j from the whole corpus' sampled fraction; the seed always counts as tau_est
+      // (the rescore reports the bound of the rows it excluded, the merge certifies)
+      const double lam = (double)k * ix->gs_frac;
+      int j = th.seed_rank ? th.seed_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
+      j = std::min(kp, std::max(1, j));
+      const int U = ix->gs_units;
+      const dim3 gw((unsigned)((nq + 3) / 4));
+      const float* um = ix->gs_umax;
+      uint32_t* tg = ix->w_taug.as<uint32_t>();
+      uint32_t* te = ix->w_tauest.as<uint32_t>();
+      if (U <= 512) hipLaunchKernelGGL(seed_select_kernel<8>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      else if (U <= 1024) hipLaunchKernelGGL(seed_select_kernel<16>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      else if (U <= 2048) hipLaunchKernelGGL(seed_select_kernel<32>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      else hipLaunchKernelGGL(seed_select_kernel<64>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      HIPC(hipGetLastError());
+    } else if (!th.no_prepass && ntiles >= (int64_t)P * min_tiles) {
       // Seed rank j.  j = k' is rigorous (k' real rows at or above the seed); a smaller j
       // estimates the global k'-th best much more tightly (the sample holds lambda = k' x
       // sampled fraction of the global top-k' on average, Poisson): j = lambda + 5 sqrt(lambda)
@@ -1129,6 +1161,20 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                              um, U, nqpad, j, M, tg, te);
         }
         HIPC(hipGetLastError());
+        if (ix->gs_sample_only) {               // the shard's sample for a global seed: done
+          ix->gs_sample_units = U;
+          ix->gs_sample_nqpad = nqpad;
+          ix->gs_sample_rows = (int64_t)a.nvt * tr_pre;
+          if (ix->timing) {                     // (the pre-pass counts in the score phase)
+            HIPC(hipEventRecord(ix->ev1, st));
+            HIPC(hipEventSynchronize(ix->ev1));
+            float ms = 0.f;
+            HIPC(hipEventElapsedTime(&ms, ix->ev0, ix->ev1));
+            ix->stats.score_kernel_ms += ms;
+            ix->stats.score_launches += 1;
+          }
+          return HCR_OK;
+        }
       } else {
         if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
         else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
@@ -1140,9 +1186,12 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
         HIPC(hipGetLastError());
       }
     }
+    if (ix->gs_sample_only) return HCR_OK;      // (no MAXONLY sample on this route: 0 units)
     const V3Launch a{nqb, P, (int)ntiles, 1, kp, unit};
     if (ix->dtype == HCR_F16) CHECK((dispatch_v3<_Float16>(ix, c3, a, cap, st)));
     else CHECK((dispatch_v3<__bf16>(ix, c3, a, cap, st)));
+  } else if (ix->gs_sample_only) {
+    return HCR_OK;
   } else if (ix->dtype == HCR_F16) CHECK((dispatch_score<_Float16, _Float16>(ix, nqb, P, ntiles, kp, cap, st)));
   else if (ix->dtype == HCR_BF16) CHECK((dispatch_score<__bf16, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
   else CHECK((dispatch_score<float, __bf16>(ix, nqb, P, ntiles, kp, cap, st)));
@@ -1591,6 +1640,94 @@ extern "C" int hcr_search_device(hcr_index* ix, const float* d_queries, int64_t 
   hipStream_t st = (hipStream_t)stream;
   if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
   return search_device_impl(ix, d_queries, nq, k, score_mode, threshold, d_out_scores, d_out_ids, st);
+}
+
+// Global seed across shards.  Step 1 on every shard: the sampling pre-pass only,
+// its unit maxima copied to d_umax as [units][nq] floats (units = 0 when this shard's route has
+// no MAXONLY sample: the caller then searches every shard the plain way).
+extern "C" int hcr_search_sample_device(hcr_index* ix, const float* d_queries, int64_t nq, int k,
+                                        float* d_umax, int64_t umax_cap, int* units,
+                                        int64_t* sampled_rows, void* stream) {
+  if (!ix || !units || !sampled_rows) return set_err(HCR_EINVAL, "NULL argument");
+  if (nq <= 0 || nq > kQueryChunk) return set_err(HCR_EINVAL, "nq %lld not in [1, %d]", (long long)nq, kQueryChunk);
+  if (k <= 0 || k > kMaxFastK) return set_err(HCR_EINVAL, "global seed: k %d not in [1, %d]", k, kMaxFastK);
+  if (!d_queries || !d_umax) return set_err(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
+  hipStream_t st = (hipStream_t)stream;
+  if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
+  *units = 0;
+  *sampled_rows = 0;
+  if (ix->n == 0) return HCR_OK;
+  ix->stats = hcr_search_stats{};
+  ix->gs_sample_only = true;
+  ix->gs_sample_units = 0;
+  ix->gs_sample_rows = 0;
+  int n_unc = 0;
+  const int rc = search_pass(ix, d_queries, (int)nq, k, HCR_SCORE_COSINE, -INFINITY, nullptr, nullptr,
+                             choose_kprime(k), st, &n_unc, nullptr);
+  ix->gs_sample_only = false;
+  CHECK(rc);
+  const int U = ix->gs_sample_units;
+  if (U == 0) return HCR_OK;
+  if ((int64_t)U * nq > umax_cap)
+    return set_err(HCR_EINVAL, "umax buffer holds %lld floats, the sample needs %d x %lld", (long long)umax_cap, U,
+                   (long long)nq);
+  // [U][nqpad] -> [U][nq]
+  const int64_t nqpad = ix->gs_sample_nqpad;
+  HIPC(hipMemcpy2DAsync(d_umax, (size_t)nq * 4, ix->w_umax.p, (size_t)nqpad * 4, (size_t)nq * 4, (size_t)U,
+                        hipMemcpyDeviceToDevice, st));
+  *units = U;
+  *sampled_rows = ix->gs_sample_rows;
+  return HCR_OK;
+}
+
+// Step 2 on every shard: the dense pass seeded from all shards' maxima (d_umax_all [units][nq],
+// sampled_fraction = the shards' sampled rows / their rows), exact fp64 scores of the shard's
+// candidates: its top k (fewer when fewer rows pass the seed: score -inf, id -1) and per query
+// the bound every other row of the shard stays at or below (d_out_bound, exact cosine; -inf =
+// none left out).  The merged list is exact where its k-th score exceeds every shard's bound.
+extern "C" int hcr_search_seeded_device(hcr_index* ix, const float* d_queries, int64_t nq, int k,
+                                        const float* d_umax_all, int units, double sampled_fraction,
+                                        double* d_out_scores, int64_t* d_out_ids, double* d_out_bound,
+                                        void* stream) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (nq <= 0 || nq > kQueryChunk) return set_err(HCR_EINVAL, "nq %lld not in [1, %d]", (long long)nq, kQueryChunk);
+  if (k <= 0 || k > kMaxFastK) return set_err(HCR_EINVAL, "global seed: k %d not in [1, %d]", k, kMaxFastK);
+  if (units <= 0 || units > 4 * 4096) return set_err(HCR_EINVAL, "units %d not in [1, 16384]", units);
+  if (!(sampled_fraction > 0.0 && sampled_fraction <= 1.0))
+    return set_err(HCR_EINVAL, "sampled_fraction %g not in (0, 1]", sampled_fraction);
+  if (!d_queries || !d_umax_all || !d_out_scores || !d_out_ids || !d_out_bound)
+    return set_err(HCR_EINVAL, "NULL buffer");
+  HIPC(hipSetDevice(ix->device));
+  CHECK(wait_ingest(ix));
+  hipStream_t st = (hipStream_t)stream;
+  if (st != ix->stream) HIPC(hipStreamSynchronize(ix->stream));
+  // (stats not reset: they accumulate over the sample + seeded pair of one search)
+  if (ix->n == 0) {
+    const int64_t tot = nq * (int64_t)k;
+    hipLaunchKernelGGL(fill_empty, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, d_out_scores,
+                       d_out_ids, tot);
+    hipLaunchKernelGGL(fill_f64, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, d_out_bound, nq,
+                       -INFINITY);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+    return HCR_OK;
+  }
+  const int kp = choose_kprime(k);
+  ix->stats.kprime = kp;
+  ix->gs_umax = d_umax_all;
+  ix->gs_units = units;
+  ix->gs_frac = sampled_fraction;
+  ix->gs_bound = d_out_bound;
+  int n_unc = 0;
+  const int rc = search_pass(ix, d_queries, (int)nq, k, HCR_SCORE_COSINE, -INFINITY, d_out_scores, d_out_ids,
+                             kp, st, &n_unc, nullptr);
+  ix->gs_umax = nullptr;
+  ix->gs_units = 0;
+  ix->gs_frac = 0.0;
+  ix->gs_bound = nullptr;
+  return rc;
 }
 
 extern "C" int hcr_search(hcr_index* ix, const float* queries, int64_t nq, int k, int score_mode,

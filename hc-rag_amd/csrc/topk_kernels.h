@@ -741,7 +741,8 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
                                               double thr, int64_t id_offset, double* __restrict__ out_s,
                                               int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
                                               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
-                                              uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap) {
+                                              uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap,
+                                              double* __restrict__ bound_out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // Every row this block dereferences (norm64, rows, idmap) comes from a candidate key.  A key
   // whose row lies outside the index can only come from a defect upstream (a score-kernel or
@@ -821,9 +822,18 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
     bool cert = true;
     const double e = eps[q];
     const uint32_t te = tau_est ? tau_est[q] : 0u;
+    double bnd = -INFINITY;                          // every excluded row's exact score is <= bnd
     if (e >= 0.0 && (nvalid >= kp || te != 0u)) {   // e < 0: zero query, exact scores all 0
       const double b = nvalid >= kp ? (double)key_score(keys[kp - 1]) : (double)unord32(te);
       cert = nvalid >= k && b + e < unord64(hi[k - 1]);
+      bnd = b + e;
+    }
+    if (bound_out) {
+      // global seed (hcr_search_seeded_device): this shard may hold fewer than k rows above
+      // the seed; it returns what it has and the bound, and the certificate moves to the merge
+      // of the shards' lists (the merged k-th best must beat every shard's bound)
+      bound_out[q] = bnd;
+      cert = true;
     }
     unc_flags[q] = cert ? 0 : 1;
     if (!cert) atomicAdd(unc_count, 1);
@@ -851,10 +861,10 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
       const double *__restrict__ norm64, int k, int mode, double thr, int64_t id_offset,            \
       double *__restrict__ out_s, int64_t *__restrict__ out_i, int *__restrict__ unc_flags,         \
       int *__restrict__ unc_count, const uint32_t *__restrict__ tau_est,                            \
-      uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap
+      uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap, double *__restrict__ bound_out
 #define HCR_RESCORE_ARGS                                                                            \
   q, kp, dim, qnorm, eps, rows, ld, n_rows, norm64, k, mode, thr, id_offset, out_s, out_i, unc_flags,      \
-      unc_count, tau_est, sk_out, idmap
+      unc_count, tau_est, sk_out, idmap, bound_out
 
 // K4 on a merged list ([q][kp] keys in global memory, merge_lists' last level).
 // LDS: dim x 8 (query) + kp x 32 + 16.

@@ -62,6 +62,10 @@ _SIGS = {
                            POINTER(c_double), POINTER(c_int64)]),
     "hcr_search_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int, c_double,
                                   c_void_p, c_void_p, c_void_p]),
+    "hcr_search_sample_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64,
+                                         POINTER(c_int), POINTER(c_int64), c_void_p]),
+    "hcr_search_seeded_device": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int,
+                                         c_double, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hcr_score_all": (c_int, [c_void_p, POINTER(c_float), c_int64, c_int, POINTER(c_double)]),
     "hcr_index_last_stats": (c_int, [c_void_p, POINTER(SearchStats)]),
     "hcr_index_set_timing": (c_int, [c_void_p, c_int]),

@@ -165,6 +165,29 @@ class VectorIndex:
                                       int(score_mode), float(threshold), c_void_p(out_scores_ptr),
                                       c_void_p(out_ids_ptr), c_void_p(stream or None)))
 
+    def sample_device(self, q_ptr: int, nq: int, k: int, umax_ptr: int, umax_cap: int,
+                      stream: int = 0):
+        """Global seed, step 1 (hcr_search_sample_device): this shard's sampled unit maxima
+        into umax_ptr ([units][nq] float32, umax_cap floats).  Returns (units, sampled_rows);
+        units == 0: no sample on this shard's route."""
+        u = ctypes.c_int(0)
+        r = ctypes.c_int64(0)
+        check(lib().hcr_search_sample_device(self._h, c_void_p(q_ptr), int(nq), int(k),
+                                             c_void_p(umax_ptr), int(umax_cap), ctypes.byref(u),
+                                             ctypes.byref(r), c_void_p(stream or None)))
+        return u.value, r.value
+
+    def search_seeded_device(self, q_ptr: int, nq: int, k: int, umax_all_ptr: int, units: int,
+                             sampled_fraction: float, out_scores_ptr: int, out_ids_ptr: int,
+                             out_bound_ptr: int, stream: int = 0) -> None:
+        """Global seed, step 3 (hcr_search_seeded_device): this shard's exact top-k among the
+        rows above the seed drawn from every shard's maxima, and per query the bound of the rest."""
+        check(lib().hcr_search_seeded_device(self._h, c_void_p(q_ptr), int(nq), int(k),
+                                             c_void_p(umax_all_ptr), int(units),
+                                             float(sampled_fraction), c_void_p(out_scores_ptr),
+                                             c_void_p(out_ids_ptr), c_void_p(out_bound_ptr),
+                                             c_void_p(stream or None)))
+
     def score_all(self, queries, score_mode: int = HCR_SCORE_COSINE) -> np.ndarray:
         """Exact fp64 cosine of every (query, row): [nq, len(self)]."""
         q = np.ascontiguousarray(np.atleast_2d(np.asarray(queries, dtype=np.float32)))

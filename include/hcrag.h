@@ -124,6 +124,32 @@ int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int 
                       int score_mode, double threshold, double* d_out_scores,
                       int64_t* d_out_ids, void* stream);
 
+/* Global seed across row shards (one index per shard: ranks of hcrag_amd.distributed or the
+ * shards of one process).  Replaces nothing in the reference (it has one corpus):
+ * it is the multi-GPU form of hcr_search_device's sampling seed, so that every shard appends
+ * only the rows above a seed drawn from the WHOLE corpus' sample instead of its own.
+ *   1. hcr_search_sample_device on every shard: its sampling pre-pass, the unit maxima copied to
+ *      d_umax as [units][nq] floats (umax_cap floats available), its sampled row count.  units =
+ *      0: this shard's route has no such sample -- search every shard with hcr_search_device.
+ *   2. the caller gathers every shard's maxima ([sum of units][nq]; pad a shard's missing units
+ *      with -INFINITY) and the sampled fraction (sum of sampled rows / sum of shard rows).
+ *   3. hcr_search_seeded_device on every shard: the dense pass from that seed; outputs the
+ *      shard's exact top k among the rows above the seed (fewer when fewer pass: score -inf, id
+ *      -1) and d_out_bound[q] (fp64): every row of the shard outside its output scores <= it
+ *      (exact cosine; -inf: none was left out).
+ *   4. merge the shards' lists (hcr_merge_topk_device): a query's merged list is the exact top
+ *      k where its k-th score is > every shard's bound; re-run the others with
+ *      hcr_search_device on every shard.
+ * Cosine scores, no threshold (score_mode COSINE, -INFINITY); 1 <= nq <= 16384, 1 <= k <= 256.
+ * hcr_index_last_stats after step 3 covers steps 1 and 3 (the seeded call adds to them). */
+int hcr_search_sample_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
+                             float* d_umax, int64_t umax_cap, int* units, int64_t* sampled_rows,
+                             void* stream);
+int hcr_search_seeded_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
+                             const float* d_umax_all, int units, double sampled_fraction,
+                             double* d_out_scores, int64_t* d_out_ids, double* d_out_bound,
+                             void* stream);
+
 /* Exact fp64 cosine of every (query, row) pair, host outputs nq x size (float64).
  * Replaces the full-score vector of experiments/isRelevant.py:206 (batch_semantic_similarity
  * returns every node's score, in node order).  Intended for small indexes. */

@@ -82,3 +82,101 @@ def test_shard_range_partitions_rows():
             rs = [shard_range(N, r, W) for r in range(W)]
             assert rs[0][0] == 0 and rs[-1][1] == N
             assert all(rs[j][1] == rs[j + 1][0] for j in range(W - 1))
+
+
+def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
+    """The global-seed protocol (ShardedSearch with local_sample / local_seeded) over gloo: the
+    stand-ins follow hcr_search_sample_device / hcr_search_seeded_device's contract -- one-row
+    sample units, the seed the j-th best of every rank's units with j from the whole corpus'
+    sampled fraction, a rank's top-k among its rows at or above the seed, and the
+    bound of the rows it left out."""
+    import math
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "hc-rag_amd")]
+    from oracle import cosine_topk as O
+    from hcrag_amd.distributed import ShardedSearch, shard_range
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    rng = np.random.default_rng(7)
+    E = rng.standard_normal((N, D))
+    E[N - 1] = E[10]                                  # duplicate across shards
+    Qall = rng.standard_normal((world * B, D)).astype(np.float32)
+    Qall[0] = E[10]
+    Qall[1::3] = E[rng.integers(0, N, Qall[1::3].shape[0])] + 0.05 * rng.standard_normal((Qall[1::3].shape[0], D))
+    r0, r1 = shard_range(N, rank, world)
+    En = E / np.linalg.norm(E, axis=1, keepdims=True)
+    stride = 4
+
+    def scores(q_all):
+        q = q_all.numpy().astype(np.float64)
+        q = q / np.linalg.norm(q, axis=1, keepdims=True)
+        # (row by row, not a GEMM: its blocking depends on the shard's shape, and a row's score
+        # must not -- duplicate rows on two shards tie exactly, as in the oracle)
+        return (q[:, None, :] * En[None, r0:r1, :]).sum(-1)          # [WB, rows]
+
+    def local_search(q_all):                         # the plain step (re-runs)
+        sc = scores(q_all)
+        o = np.argsort(-sc, axis=1, kind="stable")[:, :k]
+        return (torch.from_numpy(np.take_along_axis(sc, o, 1)),
+                torch.from_numpy((o + r0).astype(np.int64)))
+
+    def local_sample(q_all):
+        sc = scores(q_all)[:, ::stride]               # [WB, units]
+        return torch.from_numpy(np.ascontiguousarray(sc.T).astype(np.float32)), sc.shape[1]
+
+    def local_seeded(q_all, umax_all, units, frac):
+        lam = k * frac
+        j = 1 if aggressive else int(math.ceil(lam + 5 * math.sqrt(lam) + 3))
+        u = umax_all.numpy()[:units].astype(np.float64)          # [U, WB]
+        srt = -np.sort(-u, axis=0)
+        seed = srt[min(j, units) - 1] if j <= units else np.full(u.shape[1], -np.inf)
+        sc = scores(q_all)
+        WB = sc.shape[0]
+        s_out = np.full((WB, k), -np.inf)
+        i_out = np.full((WB, k), -1, dtype=np.int64)
+        bound = np.full(WB, -np.inf)
+        for q in range(WB):
+            cand = np.nonzero(sc[q] >= seed[q] - 1e-7)[0]
+            if cand.size < sc.shape[1]:
+                bound[q] = seed[q]
+            o = cand[np.lexsort((cand, -sc[q][cand]))][:k]
+            s_out[q, :o.size] = sc[q][o]
+            i_out[q, :o.size] = o + r0
+        return torch.from_numpy(s_out), torch.from_numpy(i_out), torch.from_numpy(bound)
+
+    ss = ShardedSearch(local_search, _np_merge(k), k, local_sample=local_sample,
+                       local_seeded=local_seeded, n_local=r1 - r0)
+    q_local = torch.from_numpy(Qall[rank * B:(rank + 1) * B].copy())
+    s, i = ss.search(q_local)
+    # expected: the same row-wise scores over the whole corpus, (score desc, id asc); the scores
+    # also match the oracle's
+    qn = Qall[rank * B:(rank + 1) * B].astype(np.float64)
+    qn = qn / np.linalg.norm(qn, axis=1, keepdims=True)
+    full = (qn[:, None, :] * En[None, :, :]).sum(-1)
+    ei = np.argsort(-full, axis=1, kind="stable")[:, :k]
+    es = np.take_along_axis(full, ei, 1)
+    os_, _ = O.cosine_topk(Qall[rank * B:(rank + 1) * B], E, k)
+    ok = bool(np.array_equal(i.numpy(), ei)) and bool(np.allclose(s.numpy(), es, rtol=0, atol=0)) \
+        and bool(np.allclose(s.numpy(), os_, rtol=0, atol=1e-9))
+    out[rank] = (ok, ss.last_global_seed)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,aggressive", [(2, False), (3, False), (2, True)])
+def test_sharded_search_global_seed(world, aggressive):
+    """Exact with the global seed; an over-shot seed (the best sampled unit) fails the merge
+    certificate for some queries and the step is re-run the plain way -- still exact."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_gs_worker, args=(world, port, 1201, 24, 9, 5, aggressive, out),
+                       nprocs=world, join=True, start_method="spawn")
+    res = dict(out)
+    assert all(res[r][0] for r in range(world)), res
+    reruns = {res[r][1] for r in range(world)}
+    assert len(reruns) == 1 and None not in reruns, res     # every rank took the same branch
+    if aggressive:
+        assert reruns.pop() > 0
+    else:
+        assert reruns.pop() == 0
