@@ -141,7 +141,8 @@ int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int 
  *      k where its k-th score is > every shard's bound; re-run the others with
  *      hcr_search_device on every shard.
  * Cosine scores, no threshold (score_mode COSINE, -INFINITY); 1 <= nq <= 16384, 1 <= k <= 256.
- * hcr_index_last_stats after step 3 covers steps 1 and 3 (the seeded call adds to them). */
+ * hcr_index_last_stats after step 3 covers steps 1 and 3 (the seeded call adds to them).  Step 3
+ * right after step 1 on the same index and the same d_queries reuses step 1's query preparation. */
 int hcr_search_sample_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
                              float* d_umax, int64_t umax_cap, int* units, int64_t* sampled_rows,
                              void* stream);
