@@ -2,7 +2,7 @@
 one GPU: W shard indexes of a ROWS x DIM corpus (bench.make_shard: the rows each
 rank of `bench.py --gpus W` holds), the gathered batch of GB queries (bench.make_queries).
 
-    python tools/global_seed_rank.py ROWS DIM GB K W ROUNDS
+    python tools/global_seed_rank.py ROWS DIM GB K W ROUNDS [OPT=V ...]
 
 Per round and shard: the plain per-rank search (hcr_search_device: own pre-pass, own seed) and
 the global-seed pair (hcr_search_sample_device at the shared sparser stride, then -- after the
@@ -32,6 +32,9 @@ for r in range(W):
     ix = hcrag_amd.VectorIndex(D, "f16", device=0, capacity=r1 - r0)
     bench.make_shard(ix, hcrag_amd, r0, r1, D, "f16", dev, seed=2000)
     ix.set_id_offset(r0)
+    for kv in sys.argv[7:]:                  # index options NAME=VALUE (VectorIndex.OPT_NAME)
+        name, v = kv.split("=")
+        ix.set_option(getattr(ix, "OPT_" + name), int(v))
     shards.append((ix, r0, r1))
 ix0, a0, b0 = shards[0]
 
