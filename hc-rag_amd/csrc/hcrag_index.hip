@@ -1140,10 +1140,13 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       if (maxonly) {
         const int U = 2 * a.nvt;
         CHECK(ix->w_umax.ensure((size_t)U * nqpad * 4));
-        // the sampled tiles on QW when the dense pass is QW (its MAXONLY form, score_qw.h; r03:
-        // v4's form is LDS-fill-bound), on v4 otherwise; HCR_OPT_PREPASS 1 / 2 force v4 / QW
-        // (under QS: QW's form when HCR_OPT_PREPASS = 2 on a UNIT corpus without a row mask)
-        const bool qw_pre = qw ? ix->opt_prepass != 1
+        // the sampled tiles on QW when the dense pass is QW with several query blocks (its
+        // MAXONLY form, score_qw.h; r03: v4's form is LDS-fill-bound), on v4 otherwise -- with one
+        // query block the sample is a few tiles per workgroup and QW's 256-query fragment
+        // prologue dominates them (r05pp, interleaved: configs[1] score 0.2150 -> 0.2125 ms; B =
+        // 256 at 10M x 768 a tie); HCR_OPT_PREPASS 1 / 2 force v4 / QW (under QS: QW's form when
+        // HCR_OPT_PREPASS = 2 on a UNIT corpus without a row mask)
+        const bool qw_pre = qw ? (ix->opt_prepass == 2 || (ix->opt_prepass == 0 && nqb_pre > 1))
                                : (qs && ix->opt_prepass == 2 && unit && !ix->has_mask && qw_supported(ix->ld));
         if (qw_pre) {
           QsArgs q{ix->rows.p, ix->ld, ix->n, ix->inv32.as<const float>(), nullptr, ix->w_qhat.p, nqb_pre,

@@ -625,16 +625,22 @@ __device__ __forceinline__ int merge_block_lds(const uint64_t* __restrict__ list
                                                int* s_off, int* s_hist, int* s_misc) {
   const int t = threadIdx.x;
   const int c_t = t < np ? min(cnt[(size_t)q * P + p0 + t], kp) : 0;
-  // inclusive scan of the counts (Hillis-Steele over the block)
-  s_off[t + 1] = c_t;
+  // inclusive scan of the counts: a shuffle scan per wave, then the waves' totals (two block
+  // barriers; the block-wide Hillis-Steele scan took sixteen)
+  const int lane = t & 63, wv = t >> 6;
+  int x = c_t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_misc[wv] = x;                     // (s_misc: 4 ints, 4 waves)
   if (t == 0) s_off[0] = 0;
   __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
-    const int x = t + 1 > d ? s_off[t + 1 - d] : 0;
-    __syncthreads();
-    s_off[t + 1] += x;
-    __syncthreads();
-  }
+  int base = 0;
+  for (int w = 0; w < wv; ++w) base += s_misc[w];
+  s_off[t + 1] = base + x;
+  __syncthreads();
   const int c = s_off[256];
   // flat gather: key e of the concatenation comes from the list l with s_off[l] <= e <
   // s_off[l + 1] (binary search in LDS), so all loads are independent (a wave per list

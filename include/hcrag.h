@@ -193,7 +193,8 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *                a longer pre-pass.
  *   HCR_OPT_QS_FORM: the query-stationary kernel's ring stages for 129-256 queries at D = 384:
  *                0 = the heuristic (= 3), 1 = 64-deep stages, 3 = 128-deep stages.
- *   HCR_OPT_PREPASS: the sampling pre-pass kernel: 0 = the heuristic, 1 = the 256 x 256 v4
+ *   HCR_OPT_PREPASS: the sampling pre-pass kernel: 0 = the heuristic (QW's form under a QW
+ *                dense pass of several 256-query blocks, else v4's), 1 = the 256 x 256 v4
  *                kernel's MAXONLY form, 2 = QW's MAXONLY form (also under the QS dense pass, on
  *                an L2-normalised corpus without a row mask).
  *   HCR_OPT_QW_DM: how the wide query-stationary kernel (QW) issues a row stage's LDS-DMA:

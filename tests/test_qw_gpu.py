@@ -167,10 +167,11 @@ def test_qw_cold_and_aggressive_seeds(env):
 
 @pytest.mark.parametrize("D,N", [(384, 400000 + 3), (768, 300000 + 11)])
 def test_qw_maxonly_prepass_forms_agree(hc, D, N):
-    """The sampling pre-pass on QW's MAXONLY form (HCR_OPT_PREPASS 2, the default under QW) and
-    on v4's (1): N not a multiple of the 256-row sampled tile (the last unit ends past the
-    corpus: NaN rows), several partitions of whole 128-row units; the seeds only steer which
-    rows are appended, so both give ids identical to the oracle and identical scores."""
+    """The sampling pre-pass on QW's MAXONLY form (HCR_OPT_PREPASS 2, the default under QW from
+    257 queries) and on v4's (1): N not a multiple of the 256-row sampled tile (the last unit
+    ends past the corpus: NaN rows), several partitions of whole 128-row units; the seeds only
+    steer which rows are appended, so both give ids identical to the oracle and identical
+    scores."""
     rng = np.random.default_rng(D + 7)
     B, k = 512, 16
     E = rng.standard_normal((N, D)).astype(np.float32)
