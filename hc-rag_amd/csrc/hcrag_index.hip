@@ -551,9 +551,7 @@ struct TestHooks {
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
   bool no_finish = false;            // HCRAG_NO_FINISH: separate merge + rescore launches
   bool no_mfma_filter = false;       // HCRAG_NO_MFMA_FILTER: the fallback's scans on K6 (fp64 only)
-  bool seed_from_kp = false;         // HCRAG_SEED_FROM_KP: the seed rank from k' (r04) instead of k
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
-  int finish_max = 512;              // HCRAG_FINISH_MAX: the largest batch on the fused finish_kernel
 };
 static const TestHooks& hooks() {
   static const TestHooks h = [] {
@@ -566,13 +564,11 @@ static const TestHooks& hooks() {
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
     t.no_mfma_filter = getenv("HCRAG_NO_MFMA_FILTER") != nullptr;
-    t.seed_from_kp = getenv("HCRAG_SEED_FROM_KP") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
     if (const char* e = getenv("HCRAG_SAMPLE_STRIDE")) t.sample_stride = std::max(2, atoi(e));
     if (const char* e = getenv("HCRAG_SEED_RANK")) t.seed_rank = std::max(1, atoi(e));
-    if (const char* e = getenv("HCRAG_FINISH_MAX")) t.finish_max = std::max(1, atoi(e));
     return t;
   }();
   return h;
@@ -782,6 +778,7 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
 // Merge of the last <= G lists + rescore in one launch (finish_kernel); false when its LDS
 // (the merge's keys + the fp64 query + the candidates) exceeds the CU's 160 KiB.
 static constexpr size_t kFinishDynLds = kLdsBytes - 4096;   // (its static LDS: the scan, histogram)
+static constexpr int kFinishMaxQueries = 512;     // (1024 fused: slower, r05v)
 static size_t finish_lds(int np, int kp, int dim) {
   return (size_t)next_pow2(std::max(np * kp, kp)) * 8 + (size_t)dim * 8 + (size_t)kp * 24 + 16;
 }
@@ -1129,10 +1126,10 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       // r05: lambda counts the sample's expected share of the global top-k, not top-k': the
       // seed only has to leave >= k rows above it for the short-list certificate (B = tau_est,
       // DESIGN.md §4), and a lower j halves the dense pass's appends where k' >> k (configs[1]:
-      // k = 10, k' = 64, stride 16: j 17 -> 8).  HCRAG_SEED_FROM_KP restores lambda = k' x f.
+      // k = 10, k' = 64, stride 16: j 17 -> 8).
       int j = kp;
       if (!rigorous_seed && !th.rigorous_seed) {
-        const int kseed = th.seed_from_kp ? kp : k;
+        const int kseed = k;
         const double lam = (double)kseed * ((double)a.nvt * tr_pre) / (double)ix->n;
         j = th.seed_rank ? th.seed_rank : (int)std::ceil(lam + 5.0 * std::sqrt(lam) + 3.0);
         j = std::min(kp, std::max(1, j));
@@ -1220,9 +1217,9 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
     HIPC(hipGetLastError());
   }
   // fused for small batches (configs[1], B = 256: 0.372 vs 0.376 ms per search); above
-  // 512 queries (HCRAG_FINISH_MAX) the separate launches (W = 8 rank shape, B = 1024: 1.973-1.985 vs
+  // 512 queries the separate launches (W = 8 rank shape, B = 1024: 1.973-1.985 vs
   // 1.985-1.998 ms: the fused block's merge LDS cuts the rescore's residency; r03f A/B)
-  if (!hooks().no_finish && nq <= hooks().finish_max && finish_lds(lp, kp, ix->dim) <= kFinishDynLds) {
+  if (!hooks().no_finish && nq <= kFinishMaxQueries && finish_lds(lp, kp, ix->dim) <= kFinishDynLds) {
     // the last merge level and K4 in one launch
     if (ix->dtype == HCR_F16) CHECK(launch_finish<_Float16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));
     else if (ix->dtype == HCR_BF16) CHECK(launch_finish<__bf16>(ix, merged_ptr, lcnt, lp, d_q, nq, kp, k, mode, thr, d_out_s, d_out_i, st));

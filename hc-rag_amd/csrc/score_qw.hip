@@ -19,13 +19,9 @@ namespace {
 // workgroups drift apart: 10M x 768 B = 256 3.75 vs 3.88 ms, 1M x 384 B = 256 0.266 vs 0.278 ms
 // score phase (r05c, interleaved in one process, profiles/r05/) -- and at the barrier with
 // several: spread issue lets the query blocks of a row partition drift apart, and FETCH_SIZE
-// grows 2.65x for -0.9 % at the headline (r05b/c).  HCRAG_QW_DM (0 / 3, read once) overrides.
+// grows 2.65x for -0.9 % at the headline (r05b/c).  HCR_OPT_QW_DM (0 / 3) overrides per index.
 bool qw_spread(int dm, int nqb) {
-  static const int env = [] {
-    const char* e = getenv("HCRAG_QW_DM");
-    return e ? atoi(e) : -1;
-  }();
-  const int m = dm >= 0 ? dm : env >= 0 ? env : (nqb == 1 ? 3 : 0);
+  const int m = dm >= 0 ? dm : (nqb == 1 ? 3 : 0);
   return m == 3;
 }
 
@@ -74,15 +70,10 @@ void launch_t(const QsArgs& a, hipStream_t st) {
 // 13.26 / 13.20 ms vs 13.21 / 13.38 / 13.30 with 32-row stages in a 3-deep ring) -- for batches
 // of several query blocks.  With one query block (B <= 256) every row tile comes from HBM once
 // and the 3-deep ring of 32-row stages keeps more of it in flight: 10M x 768 B = 256, 3.855 /
-// 3.859 vs 3.880 / 3.879 ms (r04h, two interleaved rounds).  HCRAG_QW_SR=32 (read once; test / A-B
-// hook) takes the 32-row form everywhere.  The MAXONLY pre-pass keeps 32-row stages (its units
-// are 128 rows).
+// 3.859 vs 3.880 / 3.879 ms (r04h, two interleaved rounds).  The MAXONLY pre-pass keeps 32-row
+// stages (its units are 128 rows).
 int dense_sr(int ks, int nqb) {
-  static const int sr = [] {
-    const char* e = getenv("HCRAG_QW_SR");
-    return e ? atoi(e) : 48;
-  }();
-  return ks == 24 && sr == 48 && nqb > 1 ? 48 : qw_sr(ks);
+  return ks == 24 && nqb > 1 ? 48 : qw_sr(ks);
 }
 
 template <typename TM, int CAP>
