@@ -426,8 +426,10 @@ extern "C" int hcr_index_set_timing(hcr_index* ix, int enable) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   HIPC(hipSetDevice(ix->device));
   if (enable && !ix->ev0) {
-    HIPC(hipEventCreate(&ix->ev0));
-    HIPC(hipEventCreate(&ix->ev1));
+    // timing only (read after the pass's own stream sync): no system-scope fence, whose cache
+    // write-back + invalidate idled the GPU ~6 us at each record (configs[1] kernel trace, r05ev)
+    HIPC(hipEventCreateWithFlags(&ix->ev0, hipEventDisableSystemFence));
+    HIPC(hipEventCreateWithFlags(&ix->ev1, hipEventDisableSystemFence));
   }
   ix->timing = enable != 0;
   return HCR_OK;
