@@ -875,15 +875,45 @@ seed_select_kernel(const float* __restrict__ umax, int U, int nqpad, int nq, int
     const float x = i < U ? umax[(size_t)i * nqpad + q] : -INFINITY;
     v[e] = (x == x && x > -INFINITY) ? ord32(x) : 0u;
   }
-  uint32_t t = 0;
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t c = t | (1u << bit);
-    int n = 0;
+  // The answer is a valid key between the smallest and largest valid one (when >= j are
+  // valid; else 0), so it shares their common prefix: the search starts below it, two bits a
+  // step (three independent ballot counts each).
+  uint32_t mx = 0u, mn = 0xFFFFFFFFu;
+  int nv = 0;
 #pragma unroll
-    for (int e = 0; e < E; ++e) n += __popcll(__ballot(v[e] >= c));
-    if (n >= j) t = c;
+  for (int e = 0; e < E; ++e) {
+    if (v[e]) { mx = v[e] > mx ? v[e] : mx; mn = v[e] < mn ? v[e] : mn; }
+    nv += __popcll(__ballot(v[e] != 0u));
   }
-  if (j > U) t = 0u;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint32_t a = (uint32_t)__shfl_xor((int)mx, m), b = (uint32_t)__shfl_xor((int)mn, m);
+    mx = a > mx ? a : mx;
+    mn = b < mn ? b : mn;
+  }
+  uint32_t t = 0u;
+  if (nv >= j) {
+    const uint32_t d = mx ^ mn;
+    int bit = d ? 31 - __clz(d) : -1;        // highest bit where the valid keys differ
+    t = bit < 0 ? mx : (mx & ~((2u << bit) - 1u));
+    for (; bit >= 1; bit -= 2) {
+      const uint32_t c1 = t | (1u << (bit - 1)), c2 = t | (2u << (bit - 1)), c3 = t | (3u << (bit - 1));
+      int n1 = 0, n2 = 0, n3 = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        n1 += __popcll(__ballot(v[e] >= c1));
+        n2 += __popcll(__ballot(v[e] >= c2));
+        n3 += __popcll(__ballot(v[e] >= c3));
+      }
+      t = n3 >= j ? c3 : n2 >= j ? c2 : n1 >= j ? c1 : t;
+    }
+    if (bit == 0) {
+      int n = 0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) n += __popcll(__ballot(v[e] >= (t | 1u)));
+      if (n >= j) t |= 1u;
+    }
+  }
   if (lane == 0) {
     tau_g[q] = t;
     if (tau_est) tau_est[q] = t;
