@@ -958,6 +958,37 @@ def main():
     if rank == 0 and world == 1 and not a.no_configs0:
         c0 = configs0_leg(hc)
 
+    # N > 1: where a step's time goes -- this rank's own search on its shard
+    # (sample + seeded, or the plain search) against the exchange (the query all-gather, the
+    # maxima all-gather, the one packed all-to-all, the merge and the re-run all-reduce), CUDA
+    # events on the step's stream over a few extra steps after the timed ones; the rank with the
+    # largest local time bounds the step.  The driver computes scaling efficiency from its own
+    # per-N values; per_rank_shape gives what its T_1 / (N T_N) needs beside them.
+    multi = None
+    if world > 1:
+        searcher.timing = True
+        ph = []
+        for _ in range(max(3, min(a.steps, 10))):
+            step()
+            ph.append(searcher.phase_ms())
+        searcher.timing = False
+        loc = torch.tensor([[p["local_ms"], p["gather_ms"], p["exchange_ms"], p["total_ms"]] for p in ph],
+                           dtype=torch.float64, device=dev).median(dim=0).values
+        allr = [torch.zeros_like(loc) for _ in range(world)]
+        dist.all_gather(allr, loc)
+        allr = torch.stack(allr).cpu().numpy()
+        multi = {"per_rank_local_ms": [round(float(x), 4) for x in allr[:, 0]],
+                 "per_rank_gather_ms": [round(float(x), 4) for x in allr[:, 1]],
+                 "per_rank_exchange_ms": [round(float(x), 4) for x in allr[:, 2]],
+                 "per_rank_step_ms": [round(float(x), 4) for x in allr[:, 3]],
+                 "local_ms": round(float(allr[:, 0].max()), 4),
+                 "exchange_ms": round(float(allr[:, 1:3].sum(axis=1).max()), 4),
+                 "collectives_per_step": searcher.collectives,
+                 "per_rank_shape": {"rows": nloc, "queries_scored": nq, "k": k},
+                 "note": "median over extra steps after the timed ones, CUDA events on the search "
+                         "stream; exchange_ms = query all-gather + maxima all-gather + packed "
+                         "all-to-all + merge + re-run decision (max over ranks); local_ms = the "
+                         "shard's own search (max over ranks)"}
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "queries/s", "n_gpus": world,
@@ -989,7 +1020,8 @@ def main():
                       "global_seed_reruns": (None if gs[0] is None else
                                              sum(x for x in gs_reruns if x is not None)),
                       "global_seed_plain_steps": (None if gs[0] is None else
-                                                  sum(1 for x in gs_reruns if x is None))},
+                                                  sum(1 for x in gs_reruns if x is None)),
+                      "multi_gpu": multi},
         }
     ix.close()
     if rank == 0 and world == 1 and not a.no_configs4:

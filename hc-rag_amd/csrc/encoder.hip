@@ -83,8 +83,9 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // HCRAG_SPLIT_NONE=1: the split GEMM in whole-tile rounds only (no K-split of the last round;
 // A/B and bit-identity tests of the other paths).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
+// HCRAG_SPLIT_DM=0|1|2|3: the split GEMM's LDS-DMA issue placement (gemm_split_kernel's DM; A/B).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  no_split = false; int streams = 0; };
+                  no_split = false; int streams = 0; int split_dm = -1; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -96,6 +97,7 @@ static const EncHooks& enc_hooks() {
     t.padded = getenv("HCRAG_ENC_PADDED") != nullptr;
     t.no_split = getenv("HCRAG_SPLIT_NONE") != nullptr;
     if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
+    if (const char* v = getenv("HCRAG_SPLIT_DM")) t.split_dm = atoi(v);
     return t;
   }();
   return h;
@@ -375,6 +377,7 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 // first and measured neutral to negative (r04n/r04o): its split ranges put the
 // workgroups that share a token tile's activations at different K offsets.
 struct SplitPlan { int ft, nft, full, rem, nsplit; };
+static constexpr int kSplitDM = 0;     // gemm_split_kernel's default DMA issue placement
 static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool split_on) {
   const int ntt = (int)(rup(T, G4_T) / G4_T);
   const int nsteps = K / V3_BK;
@@ -424,9 +427,17 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
     ws = w.split_ws.as<float>();
     cnt = w.split_cnt.as<uint32_t>();
   }
-#define HCR_SPLIT(FT_, LIB_, SP_, GRID_)                                                            \
-  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_, SP_>), dim3((unsigned)(GRID_)), dim3(V3_NT), 0, st, \
+  const int dm = enc_hooks().split_dm >= 0 ? enc_hooks().split_dm : kSplitDM;
+#define HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, DM_)                                                    \
+  hipLaunchKernelGGL((gemm_split_kernel<EPI, FT_, LIB_, SP_, DM_>), dim3((unsigned)(GRID_)), dim3(V3_NT), 0, st, \
                      W, X, K, N, T, p.nft, bias, resid, out_h, out_f, ldo, oscale, p.full, p.nsplit, ws, cnt)
+#define HCR_SPLIT(FT_, LIB_, SP_, GRID_)                                                            \
+  do {                                                                                              \
+    if (dm == 1) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 1);                                            \
+    else if (dm == 3) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 3);                                       \
+    else if (dm == 2) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 2);                                       \
+    else HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 0);                                                    \
+  } while (0)
 #define HCR_SPLIT_FT(FT_, LIB_)                                                                     \
   do {                                                                                              \
     if (p.full > 0) HCR_SPLIT(FT_, LIB_, false, p.full);                                            \
@@ -442,6 +453,7 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
   }
 #undef HCR_SPLIT_FT
 #undef HCR_SPLIT
+#undef HCR_SPLIT_DM
   HIPC(hipGetLastError());
   return HCR_OK;
 }

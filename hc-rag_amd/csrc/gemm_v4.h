@@ -323,6 +323,76 @@ __device__ __forceinline__ void g5_read8(uint32_t a, half8 (&av)[8]) {
       : "memory");
 }
 
+// every fragment of a stage (Wh, Wl', Xh, Xl'), one wait: DM = 3 reads the whole stage into
+// registers before its second barrier, which frees the slot for the stage after next
+template <int MT>
+__device__ __forceinline__ void g5_read_stage(uint32_t wh, uint32_t wl, uint32_t xh, uint32_t xl, half8 (&av)[MT],
+                                              half8 (&aw)[MT], half8 (&bq)[4], half8 (&bl)[4]) {
+  if constexpr (MT == 8) {
+    asm volatile(
+        "ds_read_b128 %0, %24\n\t"
+        "ds_read_b128 %1, %24 offset:1024\n\t"
+        "ds_read_b128 %2, %24 offset:2048\n\t"
+        "ds_read_b128 %3, %24 offset:3072\n\t"
+        "ds_read_b128 %4, %24 offset:4096\n\t"
+        "ds_read_b128 %5, %24 offset:5120\n\t"
+        "ds_read_b128 %6, %24 offset:6144\n\t"
+        "ds_read_b128 %7, %24 offset:7168\n\t"
+        "ds_read_b128 %16, %26\n\t"
+        "ds_read_b128 %17, %26 offset:1024\n\t"
+        "ds_read_b128 %18, %26 offset:2048\n\t"
+        "ds_read_b128 %19, %26 offset:3072\n\t"
+        "ds_read_b128 %20, %27\n\t"
+        "ds_read_b128 %21, %27 offset:1024\n\t"
+        "ds_read_b128 %22, %27 offset:2048\n\t"
+        "ds_read_b128 %23, %27 offset:3072\n\t"
+        "ds_read_b128 %8, %25\n\t"
+        "ds_read_b128 %9, %25 offset:1024\n\t"
+        "ds_read_b128 %10, %25 offset:2048\n\t"
+        "ds_read_b128 %11, %25 offset:3072\n\t"
+        "ds_read_b128 %12, %25 offset:4096\n\t"
+        "ds_read_b128 %13, %25 offset:5120\n\t"
+        "ds_read_b128 %14, %25 offset:6144\n\t"
+        "ds_read_b128 %15, %25 offset:7168\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(av[6]),
+          "=&v"(av[7]), "=&v"(aw[0]), "=&v"(aw[1]), "=&v"(aw[2]), "=&v"(aw[3]), "=&v"(aw[4]), "=&v"(aw[5]),
+          "=&v"(aw[6]), "=&v"(aw[7]), "=&v"(bq[0]), "=&v"(bq[1]), "=&v"(bq[2]), "=&v"(bq[3]), "=&v"(bl[0]),
+          "=&v"(bl[1]), "=&v"(bl[2]), "=&v"(bl[3])
+        : "v"(wh), "v"(wl), "v"(xh), "v"(xl)
+        : "memory");
+  } else {
+    static_assert(MT == 6, "row blocks per wave");
+    asm volatile(
+        "ds_read_b128 %0, %20\n\t"
+        "ds_read_b128 %1, %20 offset:1024\n\t"
+        "ds_read_b128 %2, %20 offset:2048\n\t"
+        "ds_read_b128 %3, %20 offset:3072\n\t"
+        "ds_read_b128 %4, %20 offset:4096\n\t"
+        "ds_read_b128 %5, %20 offset:5120\n\t"
+        "ds_read_b128 %12, %22\n\t"
+        "ds_read_b128 %13, %22 offset:1024\n\t"
+        "ds_read_b128 %14, %22 offset:2048\n\t"
+        "ds_read_b128 %15, %22 offset:3072\n\t"
+        "ds_read_b128 %16, %23\n\t"
+        "ds_read_b128 %17, %23 offset:1024\n\t"
+        "ds_read_b128 %18, %23 offset:2048\n\t"
+        "ds_read_b128 %19, %23 offset:3072\n\t"
+        "ds_read_b128 %6, %21\n\t"
+        "ds_read_b128 %7, %21 offset:1024\n\t"
+        "ds_read_b128 %8, %21 offset:2048\n\t"
+        "ds_read_b128 %9, %21 offset:3072\n\t"
+        "ds_read_b128 %10, %21 offset:4096\n\t"
+        "ds_read_b128 %11, %21 offset:5120\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(aw[0]),
+          "=&v"(aw[1]), "=&v"(aw[2]), "=&v"(aw[3]), "=&v"(aw[4]), "=&v"(aw[5]), "=&v"(bq[0]), "=&v"(bq[1]),
+          "=&v"(bq[2]), "=&v"(bq[3]), "=&v"(bl[0]), "=&v"(bl[1]), "=&v"(bl[2]), "=&v"(bl[3])
+        : "v"(wh), "v"(wl), "v"(xh), "v"(xl)
+        : "memory");
+  }
+}
+
 // FT = 256, or 192 for N = 768 (4 x 128 tiles at T = 32768 fill 2 rounds of 256 CUs exactly;
 // 256-feature tiles leave the second of 2 rounds half empty).
 __device__ __forceinline__ void g5_read6(uint32_t a, half8 (&av)[6]) {
@@ -442,7 +512,15 @@ __device__ __forceinline__ bool split_gather(floatx4 (&acc)[MT][4], char* ring, 
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
 // SPLIT = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index);
 // SPLIT = true: workgroup g is chunk g % nsplit of tile tile_base + g / nsplit (see above).
-template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false>
+// DM: where the stage's LDS-DMA pieces of stage s + 1 are issued inside stage s.  0: spread over
+// the three products (after the 1st, the 2nd and the 3rd); 1: all right after the stage barrier;
+// 2: one after each row block of the first product (Xl'.Wh), so that every piece has the 2nd and
+// 3rd products' MFMA time to land before the next stage's vmcnt(0); 3: TWO stages in flight --
+// after the stage barrier every wave reads the whole stage into registers (24 fragments), a
+// second barrier frees the slot, and the stage after next is issued into it (interleaved with the
+// first product's MFMAs); the next stage's pieces stay in flight across the whole stage (r06:
+// DM 0-2 tied at ~0.5 MFMA busy with 0.35-0.44 of the wave cycles parked at vmcnt / barrier).
+template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false, int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
                   int T_real, int n_tiles_feat, const float* __restrict__ bias,
@@ -520,6 +598,10 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   };
 #pragma unroll
   for (int i = 0; i < PPW; ++i) issue_piece(ks0, i);
+  if constexpr (DM == 3) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) issue_piece(ks0 + 1, i);
+  }
 
   const int fr = lane & 15, fc = lane >> 4;
   const int fslot = v3_slot(fc, fr);
@@ -532,8 +614,47 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   for (int s = ks0; s < ks1; ++s) {
+    if constexpr (DM == 3) {
+      // stage s landed (the PPW pieces of stage s + 1 stay in flight)
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
+      v3_barrier();
+      const char* st = ring + (s & 1) * STAGE;
+      V av[MT], aw[MT], bq[NQ], bl[NQ];
+      g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
+                        lds_addr(st + XL + offB), av, aw, bq, bl);
+      v3_barrier();               // every wave holds stage s in registers: its slot is free
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+        if (m < PPW) issue_piece(s + 2, m);
+      }
+#pragma unroll
+      for (int i = MT; i < PPW; ++i) issue_piece(s + 2, i);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NQ, 0);
+        if (m < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      if constexpr (PPW > MT) __builtin_amdgcn_sched_group_barrier(0x020, PPW - MT, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
+      continue;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
+    if constexpr (DM == 1) {
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) issue_piece(s + 1, i);
+    }
     const char* st = ring + (s & 1) * STAGE;
     V av[MT], bq[NQ], bl[NQ];
     if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
@@ -542,12 +663,28 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     g5_read4(lds_addr(st + XH + offB), bq);
     // Xl' . Wh
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m) {
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-    issue_piece(s + 1, 0);
-    issue_piece(s + 1, 1);
-    issue_piece(s + 1, 2);
+      if constexpr (DM == 2) {
+        if (m < PPW) issue_piece(s + 1, m);
+      }
+    }
+    if constexpr (DM == 2) {
+#pragma unroll
+      for (int i = MT; i < PPW; ++i) issue_piece(s + 1, i);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NQ, 0);
+        if (m < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      if constexpr (PPW > MT) __builtin_amdgcn_sched_group_barrier(0x020, PPW - MT, 0);
+    }
+    if constexpr (DM == 0) {
+      issue_piece(s + 1, 0);
+      issue_piece(s + 1, 1);
+      issue_piece(s + 1, 2);
+    }
     // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
 #pragma unroll
     for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
@@ -555,9 +692,11 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    issue_piece(s + 1, 3);
-    issue_piece(s + 1, 4);
-    issue_piece(s + 1, 5);
+    if constexpr (DM == 0) {
+      issue_piece(s + 1, 3);
+      issue_piece(s + 1, 4);
+      issue_piece(s + 1, 5);
+    }
     // Xh . Wl'
     if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
     else g5_read6(lds_addr(st + WL + offA), av);
@@ -565,8 +704,10 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    issue_piece(s + 1, 6);
-    if constexpr (PPW == 8) issue_piece(s + 1, 7);
+    if constexpr (DM == 0) {
+      issue_piece(s + 1, 6);
+      if constexpr (PPW == 8) issue_piece(s + 1, 7);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 

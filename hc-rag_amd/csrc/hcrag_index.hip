@@ -51,7 +51,13 @@ struct hcr_index {
   double gs_frac = 0.0;
   double* gs_bound = nullptr;
   const float* gs_prep_q = nullptr;   // queries the last sample call prepared (the seeded call
-  int gs_prep_nq = 0;                 // right after it, same queries, skips the prep kernel)
+  int gs_prep_nq = 0;                 // right after it, same queries, skips the prep kernel) --
+  uint64_t gs_prep_gen = 0;           // valid only while `gen` is unchanged
+  // bumped by every call that changes what a search's prep depends on (rows, rho, the unit
+  // deviation, the row mask, the route options): a prep left by a sample call is reused by the
+  // seeded call only if nothing changed in between
+  uint64_t gen = 1;
+  bool test_plant_bad_key = false;    // hcr_index_test_hook(HCR_TEST_PLANT_BAD_KEY)
   int device = 0;
   int dim = 0;
   int ld = 0;           // row stride in elements (dim rounded up to 64, zero padded)
@@ -172,6 +178,7 @@ extern "C" int hcr_index_reset(hcr_index* ix) {
   ix->has_mask = false;
   ix->has_idmap = false;
   ix->rho_dirty = true;
+  ++ix->gen;
   // on the index stream: a null-stream memset does not order against it
   HIPC(hipMemsetAsync(ix->rho.p, 0, 16, ix->stream));
   if (ix->cap > 0)
@@ -252,6 +259,7 @@ static int ingest_device(hcr_index* ix, const void* d_rows, int64_t n, int in_dt
   }
   ix->n += n;
   ix->rho_dirty = true;
+  ++ix->gen;
   return HCR_OK;
 }
 
@@ -338,6 +346,7 @@ int hcr_index_truncate_internal(hcr_index* ix, int64_t n) {
   HIPC(hipStreamSynchronize(ix->stream));
   ix->n = n;
   ix->rho_dirty = true;           // unit deviation re-measured over the rows that remain
+  ++ix->gen;
   return HCR_OK;
 }
 extern "C" int hcr_index_dim(const hcr_index* ix) { return ix ? ix->dim : -1; }
@@ -407,6 +416,7 @@ extern "C" int hcr_index_get_rows(const hcr_index* ix, int64_t row0, int64_t n, 
 extern "C" int hcr_index_set_rowmask(hcr_index* ix, const uint8_t* mask, int64_t n) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
   HIPC(hipSetDevice(ix->device));
+  ++ix->gen;
   if (!mask) { ix->has_mask = false; return HCR_OK; }
   if (n != ix->n) return set_err(HCR_EINVAL, "mask length %lld != index size %lld", (long long)n, (long long)ix->n);
   if (ix->cap == 0) { ix->has_mask = false; return HCR_OK; }
@@ -437,6 +447,10 @@ extern "C" int hcr_index_set_timing(hcr_index* ix, int enable) {
 
 extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
   if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  // every option but the sample stride can change the route, hence the prep (UNIT or not); the
+  // stride only decides which tiles the sampling pass reads (set around a sample call by
+  // distributed.hip_global_seed, between the sample and the seeded call)
+  if (option != HCR_OPT_SAMPLE_STRIDE) ++ix->gen;
   switch (option) {
     case HCR_OPT_QW1:
       if (value < -1 || value > 1) return set_err(HCR_EINVAL, "HCR_OPT_QW1 value %d not in [-1, 1]", value);
@@ -472,6 +486,13 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
     default:
       return set_err(HCR_EINVAL, "unknown index option %d", option);
   }
+}
+
+extern "C" int hcr_index_test_hook(hcr_index* ix, int hook, int value) {
+  if (!ix) return set_err(HCR_EINVAL, "index is NULL");
+  if (hook != HCR_TEST_PLANT_BAD_KEY) return set_err(HCR_EINVAL, "unknown test hook %d", hook);
+  ix->test_plant_bad_key = value != 0;
+  return HCR_OK;
 }
 
 extern "C" int hcr_index_last_stats(const hcr_index* ix, hcr_search_stats* out) {
@@ -931,7 +952,7 @@ __global__ void fill_f64(double* __restrict__ p, int64_t n, double v) {
   if (i < n) p[i] = v;
 }
 
-// HCRAG_TEST_PLANT_BAD_KEY: slot 0 of query 0's first list := the key (score 2.0, row)
+// HCR_TEST_PLANT_BAD_KEY (hcr_index_test_hook): slot 0 of query 0's first list := the key (score 2.0, row)
 __global__ void plant_key_kernel(uint64_t* __restrict__ list, int* __restrict__ cnt, uint32_t row) {
   if (threadIdx.x == 0) {
     list[0] = ((uint64_t)ord32(2.0f) << 32) | (uint64_t)(0xFFFFFFFFu - row);
@@ -1091,7 +1112,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const unsigned gq = (unsigned)((nqpad + 3) / 4);
   // (a seeded pass right after the sample call on the same queries: q^, eps and the per-query
   // state are what that call's prep left -- its pre-pass writes only the unit maxima)
-  const bool prepped = ix->gs_umax && ix->gs_prep_q == d_q && ix->gs_prep_nq == nq;
+  const bool prepped = ix->gs_umax && ix->gs_prep_q == d_q && ix->gs_prep_nq == nq && ix->gs_prep_gen == ix->gen;
   ix->gs_prep_q = nullptr;
   if (prepped) {
   } else if (tm_f16)
@@ -1128,7 +1149,18 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
       if (U <= 512) hipLaunchKernelGGL(seed_select_kernel<8>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
       else if (U <= 1024) hipLaunchKernelGGL(seed_select_kernel<16>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
       else if (U <= 2048) hipLaunchKernelGGL(seed_select_kernel<32>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
-      else hipLaunchKernelGGL(seed_select_kernel<64>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      else if (U <= 4096) hipLaunchKernelGGL(seed_select_kernel<64>, gw, dim3(256), 0, st, um, U, nq, nq, j, tg, te);
+      else {
+        // (more gathered units than 64 per lane: the block sort over all U, M = next_pow2(U) <=
+        // 16384 keys of LDS -- ADVICE r5: seed_select_kernel<64> reads only the first 4096)
+        const int M = next_pow2(U);
+        static const bool big_lds = hipFuncSetAttribute((const void*)seed_from_maxima_kernel,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        160 * 1024) == hipSuccess;
+        if (!big_lds && (size_t)M * 8 > 64 * 1024) return set_err(HCR_EHIP, "seed_from_maxima_kernel LDS attribute");
+        hipLaunchKernelGGL(seed_from_maxima_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 8, st, um, U, nq, j,
+                           M, tg, te);
+      }
       HIPC(hipGetLastError());
     } else if (!th.no_prepass && ntiles >= (int64_t)P * min_tiles) {
       // Seed rank j.  j = k' is rigorous (k' real rows at or above the seed); a smaller j
@@ -1192,6 +1224,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
           ix->gs_sample_rows = (int64_t)a.nvt * tr_pre;
           ix->gs_prep_q = d_q;
           ix->gs_prep_nq = nq;
+          ix->gs_prep_gen = ix->gen;
           if (ix->timing) {                     // (the pre-pass counts in the score phase)
             HIPC(hipEventRecord(ix->ev1, st));
             HIPC(hipEventSynchronize(ix->ev1));
@@ -1241,9 +1274,9 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   const int* lcnt = nullptr;
   int lp = 0;
   CHECK(merge_lists(ix, nq, nqpad, PL, kp, st, &merged_ptr, &lcnt, &lp));
-  // test hook (read per call, so one process can arm and disarm it): a top-scored key naming
+  // test hook (hcr_index_test_hook, per handle): a top-scored key naming
   // row n + 7 planted into query 0's first list, as a defective score kernel could leave it
-  if (getenv("HCRAG_TEST_PLANT_BAD_KEY")) {
+  if (ix->test_plant_bad_key) {
     hipLaunchKernelGGL(plant_key_kernel, dim3(1), dim3(64), 0, st, const_cast<uint64_t*>(merged_ptr),
                        const_cast<int*>(lcnt), (uint32_t)ix->n + 7u);
     HIPC(hipGetLastError());

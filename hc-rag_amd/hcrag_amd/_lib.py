@@ -70,6 +70,7 @@ _SIGS = {
     "hcr_index_last_stats": (c_int, [c_void_p, POINTER(SearchStats)]),
     "hcr_index_set_timing": (c_int, [c_void_p, c_int]),
     "hcr_index_set_option": (c_int, [c_void_p, c_int, c_int]),
+    "hcr_index_test_hook": (c_int, [c_void_p, c_int, c_int]),
     "hcr_merge_topk_device": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p,
                                       c_void_p, c_void_p]),
     "hcr_multi_create": (c_int, [c_int, POINTER(c_int), c_int, c_int, c_int64, POINTER(c_void_p)]),

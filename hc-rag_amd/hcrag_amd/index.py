@@ -227,6 +227,12 @@ class VectorIndex:
         ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 2, the default; 1 / 2 = two / one accumulator sets; 0 = off)."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
+    TEST_PLANT_BAD_KEY = 1
+
+    def test_hook(self, hook: int, value: int) -> None:
+        """Per-handle test hook (``hcr_index_test_hook``; tests only, off by default)."""
+        check(lib().hcr_index_test_hook(self._h, int(hook), int(value)))
+
 
 class MultiDeviceIndex:
     """One process, several GPUs (``hcr_multi_*``): rows sharded in

@@ -142,7 +142,11 @@ int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int 
  *      hcr_search_device on every shard.
  * Cosine scores, no threshold (score_mode COSINE, -INFINITY); 1 <= nq <= 16384, 1 <= k <= 256.
  * hcr_index_last_stats after step 3 covers steps 1 and 3 (the seeded call adds to them).  Step 3
- * right after step 1 on the same index and the same d_queries reuses step 1's query preparation. */
+ * right after step 1 on the same index and the same d_queries pointer reuses step 1's query
+ * preparation, unless the index changed in between (add, reset, truncate, row mask, options other
+ * than HCR_OPT_SAMPLE_STRIDE: the prep is then redone).  The CONTENTS of d_queries must not change
+ * between the two calls: the reuse keys on the pointer and nq, not on the values.
+ * Gathered units (step 3's `units`) up to 16384; above 4096 the seed select sorts them in LDS. */
 int hcr_search_sample_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
                              float* d_umax, int64_t umax_cap, int* units, int64_t* sampled_rows,
                              void* stream);
@@ -210,6 +214,13 @@ typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,
                HCR_OPT_QW_STAGGER = 8 } hcr_index_option;
                /* (2: removed in 0.3) */
 int hcr_index_set_option(hcr_index* index, int option, int value);
+
+/* Test hooks (tests/test_exact_gpu.py; never set in production): per handle, off by default.
+ *   HCR_TEST_PLANT_BAD_KEY: value 1 makes every later search on this handle plant a candidate
+ *                key naming a row outside the index (as a defective score kernel could): the
+ *                search must fail with HCR_EINTERNAL instead of gathering that row. */
+typedef enum { HCR_TEST_PLANT_BAD_KEY = 1 } hcr_test_hook;
+int hcr_index_test_hook(hcr_index* index, int hook, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)
  * into the global top-k (score desc, id asc).  Used after the cross-GPU exchange of

@@ -60,8 +60,10 @@ def _worker(rank, world, port, N, D, B, k, out):
     q_local = torch.from_numpy(Qall[rank * B:(rank + 1) * B].copy())
     s, i = ss.search(q_local)
     es, ei = O.cosine_topk(Qall[rank * B:(rank + 1) * B], E, k)
+    # the plain step is the query all-gather + ONE all-to-all of the packed
+    # (scores, ids) lists
     out[rank] = bool(np.array_equal(i.numpy(), ei)) and bool(
-        np.allclose(s.numpy()[ei >= 0], es[ei >= 0], rtol=0, atol=1e-12))
+        np.allclose(s.numpy()[ei >= 0], es[ei >= 0], rtol=0, atol=1e-12)) and ss.collectives == 2
     dist.destroy_process_group()
 
 
@@ -84,7 +86,7 @@ def test_shard_range_partitions_rows():
             assert all(rs[j][1] == rs[j + 1][0] for j in range(W - 1))
 
 
-def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
+def _gs_worker(rank, world, port, N, D, B, k, mode, out):
     """The global-seed protocol (ShardedSearch with local_sample / local_seeded) over gloo: the
     stand-ins follow hcr_search_sample_device / hcr_search_seeded_device's contract -- one-row
     sample units, the seed the j-th best of every rank's units with j from the whole corpus'
@@ -106,7 +108,8 @@ def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
     Qall[1::3] = E[rng.integers(0, N, Qall[1::3].shape[0])] + 0.05 * rng.standard_normal((Qall[1::3].shape[0], D))
     r0, r1 = shard_range(N, rank, world)
     En = E / np.linalg.norm(E, axis=1, keepdims=True)
-    stride = 4
+    aggressive = mode == "aggressive"
+    calls = [0]
 
     def scores(q_all):
         q = q_all.numpy().astype(np.float64)
@@ -122,6 +125,12 @@ def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
                 torch.from_numpy((o + r0).astype(np.int64)))
 
     def local_sample(q_all):
+        calls[0] += 1
+        stride = 4
+        if mode == "stale" and rank == 0 and calls[0] == 2:
+            stride = 2                                # more units than the cached shape holds
+        if mode == "raise" and rank == world - 1 and calls[0] == 2:
+            raise ValueError("over-cap sample")      # as sample_device's HcrError(EINVAL)
         sc = scores(q_all)[:, ::stride]               # [WB, units]
         return torch.from_numpy(np.ascontiguousarray(sc.T).astype(np.float32)), sc.shape[1]
 
@@ -148,7 +157,6 @@ def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
     ss = ShardedSearch(local_search, _np_merge(k), k, local_sample=local_sample,
                        local_seeded=local_seeded, n_local=r1 - r0)
     q_local = torch.from_numpy(Qall[rank * B:(rank + 1) * B].copy())
-    s, i = ss.search(q_local)
     # expected: the same row-wise scores over the whole corpus, (score desc, id asc); the scores
     # also match the oracle's
     qn = Qall[rank * B:(rank + 1) * B].astype(np.float64)
@@ -157,26 +165,46 @@ def _gs_worker(rank, world, port, N, D, B, k, aggressive, out):
     ei = np.argsort(-full, axis=1, kind="stable")[:, :k]
     es = np.take_along_axis(full, ei, 1)
     os_, _ = O.cosine_topk(Qall[rank * B:(rank + 1) * B], E, k)
-    ok = bool(np.array_equal(i.numpy(), ei)) and bool(np.allclose(s.numpy(), es, rtol=0, atol=0)) \
-        and bool(np.allclose(s.numpy(), os_, rtol=0, atol=1e-9))
-    out[rank] = (ok, ss.last_global_seed)
+    res = []
+    for _ in range(3):                                # the shape is cached after the first step
+        s, i = ss.search(q_local)
+        ok = bool(np.array_equal(i.numpy(), ei)) and bool(np.allclose(s.numpy(), es, rtol=0, atol=0)) \
+            and bool(np.allclose(s.numpy(), os_, rtol=0, atol=1e-9))
+        res.append((ok, ss.last_global_seed, ss.collectives))
+    out[rank] = res
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,aggressive", [(2, False), (3, False), (2, True)])
-def test_sharded_search_global_seed(world, aggressive):
+@pytest.mark.parametrize("world,mode", [(2, "normal"), (3, "normal"), (2, "aggressive"),
+                                        (3, "stale"), (2, "raise")])
+def test_sharded_search_global_seed(world, mode):
     """Exact with the global seed; an over-shot seed (the best sampled unit) fails the merge
-    certificate for some queries and the step is re-run the plain way -- still exact."""
+    certificate for some queries and the step is re-run the plain way -- still exact.
+    Collectives per step: the first step 5 (query all-gather, the one-time
+    shape all-reduce, maxima all-gather, ONE packed all-to-all, the re-run all-reduce), later
+    steps 4; a re-run adds 1 (its all-to-all: the queries are already gathered).
+    "stale": rank 0's second sample has more units than the cached shape -- every rank re-runs
+    that step the plain way and the third step recomputes the shape; "raise": the last rank's
+    second sample raises (an over-cap sample) -- same, without any rank raising."""
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.start_processes(_gs_worker, args=(world, port, 1201, 24, 9, 5, aggressive, out),
+    mp.start_processes(_gs_worker, args=(world, port, 1201, 24, 9, 5, mode, out),
                        nprocs=world, join=True, start_method="spawn")
     res = dict(out)
-    assert all(res[r][0] for r in range(world)), res
-    reruns = {res[r][1] for r in range(world)}
-    assert len(reruns) == 1 and None not in reruns, res     # every rank took the same branch
-    if aggressive:
-        assert reruns.pop() > 0
-    else:
-        assert reruns.pop() == 0
+    for r in range(world):
+        assert all(step[0] for step in res[r]), res   # exact on every step, every rank
+    for t in range(3):
+        steps = {res[r][t][1:] for r in range(world)}
+        assert len(steps) == 1, res                   # every rank took the same branch
+        reruns, coll = steps.pop()
+        assert reruns is not None, res
+        rerun = reruns > 0
+        expect = (5 if t == 0 or (t == 2 and mode in ("stale", "raise")) else 4) + (1 if rerun else 0)
+        assert coll == expect, (t, res)
+        if mode == "aggressive":
+            assert rerun
+        elif mode in ("stale", "raise") and t == 1:
+            assert reruns == world * 9, res          # every query of the step re-runs
+        else:
+            assert not rerun, (t, res)

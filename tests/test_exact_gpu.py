@@ -401,7 +401,7 @@ def test_normalized_16bit_store_ranks_like_the_inputs(hc, dtype):
 @pytest.mark.parametrize("B", [40, 600])                 # finish_kernel / merge + rescore_kernel
 def test_out_of_range_candidate_key_is_an_error(hc, B):
     """a candidate key naming a row outside the index (planted into query
-    0's first partition list by HCRAG_TEST_PLANT_BAD_KEY, as a defective score kernel could
+    0's first partition list by the handle's HCR_TEST_PLANT_BAD_KEY hook, as a defective score kernel could
     leave it) must fail the search with HCR_EINTERNAL -- not fault the device on the rescore's
     row gather -- and the next search on the same handle must be exact again."""
     from hcrag_amd._lib import HCR_EINTERNAL, HcrError
@@ -412,12 +412,12 @@ def test_out_of_range_candidate_key_is_an_error(hc, B):
     with hc.VectorIndex(D, "f16") as ix:
         ix.add(E, normalize=True)
         R = ix.get_rows()
-        os.environ["HCRAG_TEST_PLANT_BAD_KEY"] = "1"
+        ix.test_hook(ix.TEST_PLANT_BAD_KEY, 1)
         try:
             with pytest.raises(HcrError) as exc:
                 ix.search(Q, k)
         finally:
-            del os.environ["HCRAG_TEST_PLANT_BAD_KEY"]
+            ix.test_hook(ix.TEST_PLANT_BAD_KEY, 0)
         assert exc.value.code == HCR_EINTERNAL, exc.value
         assert "outside the index" in str(exc.value)
         s, i = ix.search(Q, k)
