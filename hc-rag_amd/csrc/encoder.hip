@@ -25,6 +25,7 @@
 
 #include "encoder_kernels.h"
 #include "gemm_v4.h"
+#include "gemm_split4.h"
 #define HCR_TOPK_TEMPLATES_ONLY   // (gemm_ws.h reaches topk_kernels.h: its kernels live in hcrag_index.hip)
 #include "gemm_ws.h"
 #include "hcrag.h"
@@ -83,9 +84,13 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // HCRAG_SPLIT_NONE=1: the split GEMM in whole-tile rounds only (no K-split of the last round;
 // A/B and bit-identity tests of the other paths).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
-// HCRAG_SPLIT_DM=0|1|2|3: the split GEMM's LDS-DMA issue placement (gemm_split_kernel's DM; A/B).
+// HCRAG_SPLIT_DM=0..4, 10 (one wave per SIMD, gemm_split4.h; 8, 9: diagnostic, wrong results): the split GEMM's LDS-DMA issue placement (gemm_split_kernel's DM; A/B).
+// HCRAG_LN_WITHX=1: the reference-precision LayerNorms also write the fp32 residual stream x
+// (r06 default: only the split activations xh, from which the O / FFN2 epilogues read the
+// residual as h + l 2^-11 -- one 4-byte-per-element write less per LayerNorm; the last layer's
+// second LayerNorm writes x for the pooling either way).
 struct EncHooks { int gemm_ft = 0; bool ln_scalar = false, gelu_liberf = false, no_ws = false, padded = false,
-                  no_split = false; int streams = 0; int split_dm = -1; };
+                  no_split = false, ln_withx = false; int streams = 0; int split_dm = -1; };
 static const EncHooks& enc_hooks() {
   static const EncHooks h = [] {
     EncHooks t;
@@ -98,6 +103,7 @@ static const EncHooks& enc_hooks() {
     t.no_split = getenv("HCRAG_SPLIT_NONE") != nullptr;
     if (const char* v = getenv("HCRAG_ENC_STREAMS")) t.streams = atoi(v);
     if (const char* v = getenv("HCRAG_SPLIT_DM")) t.split_dm = atoi(v);
+    t.ln_withx = getenv("HCRAG_LN_WITHX") != nullptr;
     return t;
   }();
   return h;
@@ -435,12 +441,21 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
   do {                                                                                              \
     if (dm == 1) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 1);                                            \
     else if (dm == 3) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 3);                                       \
+    else if (dm == 4) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 4);                                       \
+    else if (dm == 8) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 8);                                       \
+    else if (dm == 9) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 9);                                       \
     else if (dm == 2) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 2);                                       \
     else HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 0);                                                    \
   } while (0)
 #define HCR_SPLIT_FT(FT_, LIB_)                                                                     \
   do {                                                                                              \
-    if (p.full > 0) HCR_SPLIT(FT_, LIB_, false, p.full);                                            \
+    if (p.full > 0) {                                                                               \
+      if (dm == 10 && FT_ == G4_T)                                                                  \
+        hipLaunchKernelGGL((gemm_split4_kernel<EPI, LIB_>), dim3((unsigned)p.full), dim3(256), 0, st, W, X, K, N, T, \
+                           p.nft, bias, resid, out_h, out_f, ldo, oscale);                          \
+      else                                                                                          \
+        HCR_SPLIT(FT_, LIB_, false, p.full);                                                        \
+    }                                                                                               \
     if (p.nsplit > 0) HCR_SPLIT(FT_, LIB_, true, p.rem * p.nsplit);                                 \
   } while (0)
   if constexpr (!can192) {
@@ -580,11 +595,14 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
   const unsigned gT = (unsigned)((T + 3) / 4);
   // vectorised LayerNorm kernels when H % 4 == 0 and H <= 1024 (all BERT widths here)
   const bool ln4 = (H % 4 == 0) && H <= 1024 && !enc_hooks().ln_scalar;
-  auto layer_norm = [&](const DevBuf& g, const DevBuf& bb) {
+  // reference precision: the residual stream lives in xh only (EPI_BIAS_RESID_XH), x is written
+  // by the last LayerNorm for the pooling
+  const bool nox = SPLIT && ln4 && !enc_hooks().ln_withx;
+  auto layer_norm = [&](const DevBuf& g, const DevBuf& bb, bool last) {
     if (ln4)
       hipLaunchKernelGGL((layernorm4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, w.y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
-                         w.x.as<float>(), w.xh.as<TM>());
+                         (nox && !last) ? nullptr : w.x.as<float>(), w.xh.as<TM>());
     else
       hipLaunchKernelGGL((layernorm_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, w.y.as<const float>(),
                          (int)T, H, g.as<const float>(), bb.as<const float>(), c.layer_norm_eps,
@@ -594,7 +612,8 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
     hipLaunchKernelGGL((embed_ln4_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
                        e->temb.as<const float>(), e->embg.as<const float>(),
-                       e->embb.as<const float>(), c.layer_norm_eps, w.x.as<float>(), w.xh.as<TM>());
+                       e->embb.as<const float>(), c.layer_norm_eps, nox ? nullptr : w.x.as<float>(),
+                       w.xh.as<TM>());
   else
     hipLaunchKernelGGL((embed_ln_kernel<TM, SPLIT>), dim3(gT), dim3(256), 0, st, d_ids, tok_map, (int)T, S, H,
                        e->wemb.as<const float>(), e->pemb.as<const float>(),
@@ -614,15 +633,22 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
                                        3 * H, L.sqkv, st)));
       CHECK(launch_attention<TM>(e, w, key_mask, seq_off, n, S, st));
     }
-    if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H, H,
-                                               (int)T, L.bo.as<const float>(), w.x.as<const float>(),
-                                               nullptr, w.y.as<float>(), H, L.so, st)));
+    if constexpr (SPLIT) {
+      if (nox)
+        CHECK((launch_gemm_split<EPI_BIAS_RESID_XH>(w, e->ncu, L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H,
+                                                    H, (int)T, L.bo.as<const float>(),
+                                                    reinterpret_cast<const float*>(w.xh.p), nullptr, w.y.as<float>(),
+                                                    H, L.so, st)));
+      else
+        CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo.as<const _Float16>(), w.ctx.as<const _Float16>(), H,
+                                                 H, (int)T, L.bo.as<const float>(), w.x.as<const float>(),
+                                                 nullptr, w.y.as<float>(), H, L.so, st)));
+    }
     else
       CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo.as<const TM>(), w.ctx.as<const TM>(), H, H,
                                              (int)T, L.bo.as<const float>(), w.x.as<const float>(),
                                              nullptr, w.y.as<float>(), H, L.so, st)));
-    layer_norm(L.ln1g, L.ln1b);
+    layer_norm(L.ln1g, L.ln1b, false);
     HIPC(hipGetLastError());
     if constexpr (SPLIT)
       CHECK((launch_gemm_split<EPI_BIAS_GELU_SPLIT>(w, e->ncu, L.wi.as<const _Float16>(), w.xh.as<const _Float16>(),
@@ -632,15 +658,22 @@ static int encode_t(hcr_encoder* e, EncWork& w, const int32_t* d_ids, const int3
       CHECK((launch_gemm<TM, EPI_BIAS_GELU>(L.wi.as<const TM>(), w.xh.as<const TM>(), H, F, (int)T,
                                             L.bi.as<const float>(), nullptr, w.inter.as<TM>(),
                                             nullptr, F, L.si, st)));
-    if constexpr (SPLIT)
-      CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(), F,
-                                               H, (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
-                                               nullptr, w.y.as<float>(), H, L.so2, st)));
+    if constexpr (SPLIT) {
+      if (nox)
+        CHECK((launch_gemm_split<EPI_BIAS_RESID_XH>(w, e->ncu, L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(),
+                                                    F, H, (int)T, L.bo2.as<const float>(),
+                                                    reinterpret_cast<const float*>(w.xh.p), nullptr, w.y.as<float>(),
+                                                    H, L.so2, st)));
+      else
+        CHECK((launch_gemm_split<EPI_BIAS_RESID>(w, e->ncu, L.wo2.as<const _Float16>(), w.inter.as<const _Float16>(), F,
+                                                 H, (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
+                                                 nullptr, w.y.as<float>(), H, L.so2, st)));
+    }
     else
       CHECK((launch_gemm<TM, EPI_BIAS_RESID>(L.wo2.as<const TM>(), w.inter.as<const TM>(), F, H,
                                              (int)T, L.bo2.as<const float>(), w.x.as<const float>(),
                                              nullptr, w.y.as<float>(), H, L.so2, st)));
-    layer_norm(L.ln2g, L.ln2b);
+    layer_norm(L.ln2g, L.ln2b, l == c.layers - 1);
     HIPC(hipGetLastError());
   }
   hipLaunchKernelGGL(pool_normalize_kernel, dim3((unsigned)n), dim3(256), 0, st,

@@ -112,7 +112,7 @@ __device__ __forceinline__ void ln_row4(float4 (&v)[4], int H, const float* __re
     o.y = (v[i].y - mean) * rstd * gg.y + bb.y;
     o.z = (v[i].z - mean) * rstd * gg.z + bb.z;
     o.w = (v[i].w - mean) * rstd * gg.w + bb.w;
-    reinterpret_cast<float4*>(xo)[d4] = o;
+    if (xo) reinterpret_cast<float4*>(xo)[d4] = o;    // (NULL: the residual stream is read from xh)
     store_act4<TM, SPLIT>(xho, H, 4 * d4, o);
   }
 }
@@ -129,7 +129,7 @@ layernorm4_kernel(const float* __restrict__ y, int T_real, int H, const float* _
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     v[i] = (lane + 64 * i < (H >> 2)) ? yr[lane + 64 * i] : float4{0.f, 0.f, 0.f, 0.f};
-  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x + (size_t)t * H,
+  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x ? x + (size_t)t * H : nullptr,
                      xh + (size_t)t * H * act_width<SPLIT>());
 }
 
@@ -158,7 +158,7 @@ embed_ln4_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ to
       v[i] = float4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x + (size_t)t * H,
+  ln_row4<TM, SPLIT>(v, H, g, b, eps, lane, x ? x + (size_t)t * H : nullptr,
                      xh + (size_t)t * H * act_width<SPLIT>());
 }
 
@@ -200,8 +200,11 @@ layernorm_kernel(const float* __restrict__ y, int T_real, int H, const float* __
 //   EPI_BIAS_F32        -> fp32 out_f [T][ldo]                         (split QKV)
 //   EPI_BIAS_GELU_SPLIT -> exact-erf GELU, split out_h [T][3 ldo]      (split FFN1)
 // -------------------------------------------------------------------------------------
+//   EPI_BIAS_RESID_XH   -> + resid from the split activations (h + l 2^-11 of [T][3 ldo] f16),
+//                          fp32 out_f [T][ldo]   (split O-proj / FFN2 when the LayerNorms do not
+//                          write the fp32 residual stream, r06)
 enum : int { EPI_BIAS = 0, EPI_BIAS_GELU = 1, EPI_BIAS_RESID = 2, EPI_BIAS_F32 = 3,
-             EPI_BIAS_GELU_SPLIT = 4 };
+             EPI_BIAS_GELU_SPLIT = 4, EPI_BIAS_RESID_XH = 5 };
 
 // GELU(x) = x/2 (1 + erf(x / sqrt 2)) (HF BERT "gelu", exact-erf form).  erf by Abramowitz &
 // Stegun 7.1.26 (|error| <= 1.5e-7, far below the fp16/bf16 output rounding) on v_rcp / v_exp:

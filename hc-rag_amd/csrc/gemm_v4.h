@@ -64,6 +64,18 @@ __device__ __forceinline__ void staged_epilogue_f32(char* vs, int lane, const fl
       if constexpr (EPI == EPI_BIAS_RESID)
         rr[i] = *reinterpret_cast<const float4*>(resid + (size_t)min(t, T_real - 1) * ldo +
                                                  min(fcol, N_real - 4));
+      if constexpr (EPI == EPI_BIAS_RESID_XH) {
+        // the residual stream as the LayerNorm left it in the split activations: h + l 2^-11
+        // ([T][3 ldo] f16, h at column f, l at 2 ldo + f; |x - h - l 2^-11| <= |x| 2^-23)
+        const _Float16* xr = reinterpret_cast<const _Float16*>(resid) + (size_t)min(t, T_real - 1) * 3 * ldo +
+                             min(fcol, N_real - 4);
+        union { uint2 u; _Float16 e[4]; } h, l;
+        h.u = *reinterpret_cast<const uint2*>(xr);
+        l.u = *reinterpret_cast<const uint2*>(xr + 2 * ldo);
+        constexpr float r = 1.f / kSplitLo;
+        rr[i] = float4{fmaf((float)l.e[0], r, (float)h.e[0]), fmaf((float)l.e[1], r, (float)h.e[1]),
+                       fmaf((float)l.e[2], r, (float)h.e[2]), fmaf((float)l.e[3], r, (float)h.e[3])};
+      }
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -508,6 +520,63 @@ __device__ __forceinline__ bool split_gather(floatx4 (&acc)[MT][4], char* ring, 
   return true;
 }
 
+// FFN1 (reference-precision mode): the split activations (h, l) of a wave's 128 features x 64
+// tokens go out through LDS.  Stored straight from the accumulators a lane writes 4 features of
+// one token: 32-B pieces of 16 different rows per instruction, half-line writes on ~400 MB per
+// launch.  Here the wave stages 64 features x 64 tokens of h and of l (8 KiB each, 16-B granules
+// XOR-swizzled by token) in its 16 KiB at `hs`, then writes 128-B row pieces: 8 lanes per token
+// row.  fbase / tbase: the wave's first feature / token.
+template <bool LIBERF>
+__device__ __forceinline__ void ffn1_split_epilogue(char* hs, int lane, const floatx4 (&acc)[8][4], int fbase,
+                                                    int tbase, int N_real, int T_real,
+                                                    const float* __restrict__ bias, _Float16* __restrict__ out_h,
+                                                    int ldo, float oscale) {
+  char* ls = hs + 8192;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int m = hh * 4 + mi;
+      const int fl = mi * 16 + (lane >> 4) * 4;               // feature within the 64
+      const float4 bb = *reinterpret_cast<const float4*>(bias + fbase + hh * 64 + fl);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int tl = n * 16 + (lane & 15);                  // token within the 64
+        float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
+                      fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
+        union { _Float16 e[4]; uint2 u; } ph, pl;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = LIBERF ? gelu_exact(v[r]) : gelu_erf(v[r]);
+          ph.e[r] = (_Float16)v[r];
+          pl.e[r] = (_Float16)((v[r] - (float)ph.e[r]) * kSplitLo);
+        }
+        const int off = tl * 128 + (((fl >> 3) ^ (tl & 7)) << 4) + (fl & 7) * 2;
+        *reinterpret_cast<uint2*>(hs + off) = ph.u;
+        *reinterpret_cast<uint2*>(ls + off) = pl.u;
+      }
+    }
+    wave_lds_sync();
+    // 64 rows x 8 granules: 8 rows per instruction, lane -> (row lane / 8, granule lane % 8)
+    const int gr = lane & 7;
+    const int fcol = fbase + hh * 64 + gr * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int tl = i * 8 + (lane >> 3);
+      const int t = tbase + tl;
+      const int off = tl * 128 + ((gr ^ (tl & 7)) << 4);
+      const uint4 h4 = *reinterpret_cast<const uint4*>(hs + off);
+      const uint4 l4 = *reinterpret_cast<const uint4*>(ls + off);
+      if (t < T_real && fcol < N_real) {
+        _Float16* row = out_h + (size_t)t * 3 * ldo;
+        *reinterpret_cast<uint4*>(row + fcol) = h4;
+        *reinterpret_cast<uint4*>(row + 2 * ldo + fcol) = l4;
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // LIBERF: the FFN1 epilogue's GELU with the library erff (~50 instructions) instead of erf_as
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
 // SPLIT = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index);
@@ -598,7 +667,7 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   };
 #pragma unroll
   for (int i = 0; i < PPW; ++i) issue_piece(ks0, i);
-  if constexpr (DM == 3) {
+  if constexpr (DM >= 3 && DM != 9) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) issue_piece(ks0 + 1, i);
   }
@@ -613,7 +682,80 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // DM 8 / 9: DIAGNOSTIC ONLY (wrong results; HCRAG_SPLIT_DM, tools/enc_prof.py timing): DM 4's
+  // loop without the LDS fragment reads after the first stage (8) or without the stage DMA (9)
+  V d_av[MT], d_aw[MT], d_bq[NQ], d_bl[NQ];
+  if constexpr (DM == 8) {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
+    v3_barrier();
+    g5_read_stage<MT>(lds_addr(ring + WH + offA), lds_addr(ring + WL + offA), lds_addr(ring + XH + offB),
+                      lds_addr(ring + XL + offB), d_av, d_aw, d_bq, d_bl);
+  }
   for (int s = ks0; s < ks1; ++s) {
+    if constexpr (DM == 8 || DM == 9) {
+      if constexpr (DM == 8) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
+      v3_barrier();
+      V av[MT], aw[MT], bq[NQ], bl[NQ];
+      if constexpr (DM == 9) {
+        const char* st = ring + (s & 1) * STAGE;
+        g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
+                          lds_addr(st + XL + offB), av, aw, bq, bl);
+      } else {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) { av[m] = d_av[m]; aw[m] = d_aw[m]; }
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) { bq[n] = d_bq[n]; bl[n] = d_bl[n]; }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(av[m]), "+v"(aw[m]));
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) asm volatile("" : "+v"(bq[n]), "+v"(bl[n]));
+      }
+      v3_barrier();
+      V as[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) as[m] = av[m] * (_Float16)2048.0f;
+      constexpr int NM = 3 * MT * NQ, GAP = NM / PPW;
+#pragma unroll
+      for (int u = 0; u < NM; ++u) {
+        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
+        if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+        else if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
+        else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
+        if constexpr (DM == 8)
+          if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
+      }
+      continue;
+    }
+    if constexpr (DM == 4) {
+      // DM 3's two stages in flight with the PPW pieces spread evenly over all 3 x MT x NQ
+      // MFMAs of the stage (one per ~12): the CU's vector-memory path sees an even demand
+      // instead of a burst per product
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
+      v3_barrier();
+      const char* st = ring + (s & 1) * STAGE;
+      V av[MT], aw[MT], bq[NQ], bl[NQ];
+      g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
+                        lds_addr(st + XL + offB), av, aw, bq, bl);
+      v3_barrier();
+      V as[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) as[m] = av[m] * (_Float16)2048.0f;
+      constexpr int NM = 3 * MT * NQ, GAP = NM / PPW;
+#pragma unroll
+      for (int u = 0; u < NM; ++u) {
+        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
+        if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+        else if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
+        else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
+        if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
+      }
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, GAP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      continue;
+    }
     if constexpr (DM == 3) {
       // stage s landed (the PPW pieces of stage s + 1 stay in flight)
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
@@ -720,60 +862,12 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
 
   if constexpr (EPI == EPI_BIAS_GELU_SPLIT) {
     static_assert(FT == 256, "the FFN1 epilogue stages 64-feature halves of a 128-feature wave");
-    // FFN1: the split activations (h, l) go out through LDS.  Stored straight from the
-    // accumulators a lane writes 4 features of one token: 32-B pieces of 16 different rows per
-    // instruction, half-line writes on ~400 MB per launch.  Here each wave stages 64 features x
-    // 64 tokens of h and of l (8 KiB each, 16-B granules XOR-swizzled by token) in its 16 KiB of
-    // the now idle ring, then writes 128-B row pieces: 8 lanes per token row.
     __syncthreads();                               // every wave done with the ring
-    char* hs = ring + wave * 16384;
-    char* ls = hs + 8192;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int m = hh * 4 + mi;
-        const int fl = mi * 16 + (lane >> 4) * 4;               // feature within the 64
-        const float4 bb = *reinterpret_cast<const float4*>(bias + f0 + wm * 128 + hh * 64 + fl);
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-          const int tl = n * 16 + (lane & 15);                  // token within the 64
-          float v[4] = {fmaf(acc[m][n][0], oscale, bb.x), fmaf(acc[m][n][1], oscale, bb.y),
-                        fmaf(acc[m][n][2], oscale, bb.z), fmaf(acc[m][n][3], oscale, bb.w)};
-          union { _Float16 e[4]; uint2 u; } ph, pl;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = LIBERF ? gelu_exact(v[r]) : gelu_erf(v[r]);
-            ph.e[r] = (_Float16)v[r];
-            pl.e[r] = (_Float16)((v[r] - (float)ph.e[r]) * kSplitLo);
-          }
-          const int off = tl * 128 + (((fl >> 3) ^ (tl & 7)) << 4) + (fl & 7) * 2;
-          *reinterpret_cast<uint2*>(hs + off) = ph.u;
-          *reinterpret_cast<uint2*>(ls + off) = pl.u;
-        }
-      }
-      wave_lds_sync();
-      // 64 rows x 8 granules: 8 rows per instruction, lane -> (row lane / 8, granule lane % 8)
-      const int gr = lane & 7;
-      const int fcol = f0 + wm * 128 + hh * 64 + gr * 8;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int tl = i * 8 + (lane >> 3);
-        const int t = t0 + wn * 64 + tl;
-        const int off = tl * 128 + ((gr ^ (tl & 7)) << 4);
-        const uint4 h4 = *reinterpret_cast<const uint4*>(hs + off);
-        const uint4 l4 = *reinterpret_cast<const uint4*>(ls + off);
-        if (t < T_real && fcol < N_real) {
-          _Float16* row = out_h + (size_t)t * 3 * ldo;
-          *reinterpret_cast<uint4*>(row + fcol) = h4;
-          *reinterpret_cast<uint4*>(row + 2 * ldo + fcol) = l4;
-        }
-      }
-      wave_lds_sync();
-    }
+    ffn1_split_epilogue<LIBERF>(ring + wave * 16384, lane, acc, f0 + wm * 128, t0 + wn * 64, N_real, T_real,
+                                bias, out_h, ldo, oscale);
   } else {
     // fp32 outputs (QKV: bias; O / FFN2: bias + residual) through LDS as well
-    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID, "split GEMM epilogues");
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_RESID_XH, "split GEMM epilogues");
     __syncthreads();                               // every wave done with the ring
     staged_epilogue_f32<EPI, MT>(ring + wave * 8192, lane, acc, f0 + wm * (FT / 2), t0 + wn * 64,
                                  N_real, T_real, bias, resid, out_f, ldo, oscale);

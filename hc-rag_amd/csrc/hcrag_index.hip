@@ -78,7 +78,7 @@ struct hcr_index {
       w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
-      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est;
+      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est, f_sorth, f_sortl;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
@@ -159,7 +159,7 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
-                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est};
+                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est, &ix->f_sorth, &ix->f_sortl};
   for (DevBuf* b : all) b->release();
   if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
@@ -1343,13 +1343,33 @@ static constexpr int kMaxK = 2048;            // kFallbackCap > k: every K7 roun
 // Exact top-k of the chunk-local queries `idx` of the m x dim device queries `qc` by one fp64
 // scan of every row (a K6/K7 round per threshold); results go to rows idx[i] of os / oi.
 // sk[i]: the starting threshold (K4's s_k of the candidates; 0 = every row).
+// Deep path (k > kMaxK, r06: K7b + the bitonic segment sort of deep_sort.hip): `cap` > K7's
+// 8192 LDS slots; the select step finds the exact k-th admitted key by a radix select and only
+// the k answers are sorted.
+int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStream_t st);   // deep_sort.hip
+int hcr_launch_select_big(int nq, int k, int cap, int P, const unsigned int* cnt, const uint64_t* buf_hi,
+                          const uint64_t* buf_lo, uint64_t* th_hi, uint64_t* th_lo, int* active, int* n_again,
+                          double* h_lo, double* h_hi, const unsigned int* h_cnt, const unsigned long long* h_min,
+                          int* est, uint64_t* sort_hi, uint64_t* sort_lo, hipStream_t st);
+int hcr_launch_deep_emit(int nq, const uint64_t* sh, const uint64_t* sl, int P, int k, int mode, double thr,
+                         int64_t id_offset, const int64_t* idmap, const int* out_idx, double* out_s, int64_t* out_i,
+                         hipStream_t st);
+int hcr_merge_sorted(const double* d_scores, const int64_t* d_ids, int g, int64_t nq, int k, double* d_out_scores,
+                     int64_t* d_out_ids, hipStream_t st);
+static constexpr size_t kDeepBudget = (size_t)2 << 30;   // admission + sort buffers of a deep group
+
 static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>& idx,
                           const std::vector<uint64_t>& sk, int k, int mode, double thr, double* os,
-                          int64_t* oi, hipStream_t st) {
-  const int cap = kFallbackCap;
-  const size_t sel_lds = (size_t)2 * cap * 8;
-  HIPC(hipFuncSetAttribute((const void*)exact_select_kernel,
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+                          int64_t* oi, hipStream_t st, int64_t cap64 = kFallbackCap) {
+  const bool big = cap64 > kFallbackCap;
+  const int cap = (int)cap64;
+  const size_t sel_lds = (size_t)2 * kFallbackCap * 8;
+  if (!big)
+    HIPC(hipFuncSetAttribute((const void*)exact_select_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+  // the deep path's sort buffers: P = a power of two >= the most answers a query can have
+  int P = 2;
+  while (big && P < std::min<int64_t>(k, std::max<int64_t>(ix->n, 1))) P <<= 1;
   // the MFMA prefilter (K6m, and K6h for queries without a starting threshold) for 16-bit rows
   // at ld = 384 / 768 / 1024; K6 (an fp64 dot per row and query) otherwise
   const int ksteps = ix->ld / 32;
@@ -1358,7 +1378,12 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   if (mf) CHECK(refresh_norm_stats(ix));
   // MFMA-prefiltered scans take up to kFbGroupsPerScan query groups at once (one pass over the
   // rows for all of them); the fp64 scan (K6) one group
-  const int super = mf ? kFallbackGroup * kFbGroupsPerScan : kFallbackGroup;
+  int super = mf ? kFallbackGroup * kFbGroupsPerScan : kFallbackGroup;
+  if (big) {             // (the deep path's buffers per query: cap admitted + P sorted pairs)
+    const int64_t per_q = (cap64 + P) * 16;
+    const int64_t fit = std::max<int64_t>(1, (int64_t)(kDeepBudget / (size_t)per_q));
+    super = (int)std::min<int64_t>(super, fit >= kFallbackGroup ? fit / kFallbackGroup * kFallbackGroup : fit);
+  }
   const int64_t mchunks = round_up(std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32, 2048)), 8);
 #define MFIL(TS, KS, HIST)                                                                        \
   hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, HIST>), dim3((unsigned)(mchunks * ngr)), dim3(256), 0, st, \
@@ -1394,6 +1419,10 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     CHECK(ix->f_cnt.ensure((size_t)ng * 4));
     CHECK(ix->f_bufh.ensure((size_t)ng * cap * 8));
     CHECK(ix->f_bufl.ensure((size_t)ng * cap * 8));
+    if (big) {
+      CHECK(ix->f_sorth.ensure((size_t)ng * P * 8));
+      CHECK(ix->f_sortl.ensure((size_t)ng * P * 8));
+    }
     CHECK(ix->f_again.ensure(16));
     CHECK(ix->f_hlo.ensure((size_t)ng * 8));
     CHECK(ix->f_hhi.ensure((size_t)ng * 8));
@@ -1511,19 +1540,36 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
       if (mf) launch_mfil(ng, false, 1);
       else if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
 #undef FIL
-      hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
-                         ix->f_cnt.as<const unsigned int>(), ix->f_bufh.as<const uint64_t>(),
-                         ix->f_bufl.as<const uint64_t>(), ix->f_thh.as<uint64_t>(),
-                         ix->f_thl.as<uint64_t>(), ix->f_act.as<int>(), ix->f_again.as<int>(), mode,
-                         thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
-                         ix->f_idx.as<const int>(), os, oi, ix->f_hlo.as<double>(),
-                         ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
-                         ix->f_hmin.as<const unsigned long long>(), ix->f_est.as<int>());
+      if (big)
+        CHECK(hcr_launch_select_big(ng, k, cap, P, ix->f_cnt.as<const unsigned int>(), ix->f_bufh.as<const uint64_t>(),
+                                    ix->f_bufl.as<const uint64_t>(), ix->f_thh.as<uint64_t>(), ix->f_thl.as<uint64_t>(),
+                                    ix->f_act.as<int>(), ix->f_again.as<int>(), ix->f_hlo.as<double>(),
+                                    ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
+                                    ix->f_hmin.as<const unsigned long long>(), ix->f_est.as<int>(),
+                                    ix->f_sorth.as<uint64_t>(), ix->f_sortl.as<uint64_t>(), st));
+      else
+        hipLaunchKernelGGL(exact_select_kernel, dim3(ng), dim3(256), sel_lds, st, k, cap,
+                           ix->f_cnt.as<const unsigned int>(), ix->f_bufh.as<const uint64_t>(),
+                           ix->f_bufl.as<const uint64_t>(), ix->f_thh.as<uint64_t>(),
+                           ix->f_thl.as<uint64_t>(), ix->f_act.as<int>(), ix->f_again.as<int>(), mode,
+                           thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
+                           ix->f_idx.as<const int>(), os, oi, ix->f_hlo.as<double>(),
+                           ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
+                           ix->f_hmin.as<const unsigned long long>(), ix->f_est.as<int>());
       HIPC(hipGetLastError());
       HIPC(hipMemcpyAsync(&again, ix->f_again.p, 4, hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
     }
     ix->stats.fallback_rounds += rounds;
+    if (big) {             // every query of the group holds its k answers: sort them, emit
+      CHECK(hcr_seg_sort_desc_pairs(ix->f_sorth.as<uint64_t>(), ix->f_sortl.as<uint64_t>(), ng, P, st));
+      CHECK(hcr_launch_deep_emit(ng, ix->f_sorth.as<const uint64_t>(), ix->f_sortl.as<const uint64_t>(), P, k, mode,
+                                 thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
+                                 ix->f_idx.as<const int>(), os, oi, st));
+      // (K7 writes its outputs inside the round loop, before its stream sync; these come after
+      // it: the outputs are final when the search call returns, hcrag.h)
+      HIPC(hipStreamSynchronize(st));
+    }
   }
 #undef MFIL_KS
 #undef MFIL
@@ -1531,81 +1577,22 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
 }
 
 // ---- deep top-k: k > kMaxK (the fallback's LDS select holds 8192 slots) ----
-// Every row's exact key per query, sorted per query by a stable segmented radix sort (score
-// desc; rows enter in ascending order, so ties stay row asc), the first k kept.  For the
-// reference's argsort(...)[::-1][:top_k] at any top_k (experiments/main.py:844,889).  Query
-// groups are sized so that keys + rows (in and out) stay within kDeepBudget bytes.
-int hcr_seg_sort_u64_u32(DevBuf& temp, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
-                         uint32_t* vout, int num_items, int num_segments, const int* offs,
-                         int descending, hipStream_t st);              // deep_sort.hip
-static constexpr size_t kDeepBudget = (size_t)4 << 30;
-
-__global__ void seg_offsets_kernel(int* __restrict__ offs, int nseg, int len) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= nseg) offs[i] = i * len;
-}
-
-__global__ void deep_out_kernel(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ vals,
-                                int64_t n, int k, int mode, double thr, int64_t id_offset,
-                                const int64_t* __restrict__ idmap, double* __restrict__ out_s,
-                                int64_t* __restrict__ out_i) {
-  const int q = blockIdx.y;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    double s = -INFINITY;
-    int64_t id = -1;
-    if (t < n) {
-      const uint64_t key = keys[(int64_t)q * n + t];
-      if (key) {
-        double v = unord64(key);
-        if (mode == 1) v = (v + 1.0) / 2.0;
-        if (v >= thr) { s = v; id = row_id(id_offset, idmap, vals[(int64_t)q * n + t]); }
-      }
-    }
-    out_s[(int64_t)q * k + t] = s;
-    out_i[(int64_t)q * k + t] = id;
-  }
-}
-
+// The exact fallback with admission buffers of cap = a power of two >= 4k slots per query (K6h's
+// threshold admits ~k rows plus one histogram bin's worth; an overflow tightens it), the k-th
+// best admitted key by a radix select, and a bitonic sort of the k answers (deep_sort.hip).  For
+// the reference's argsort(...)[::-1][:top_k] at any top_k (experiments/main.py:844,889).
 static int deep_topk(hcr_index* ix, const float* qc, int m, int k, int mode, double thr, double* os,
                      int64_t* oi, hipStream_t st) {
-  const int64_t n = ix->n;
-  if (n > INT32_MAX) return set_err(HCR_EINVAL, "k > %d needs an index of < 2^31 rows", kMaxK);
-  int64_t G = std::min<int64_t>(m, std::max<int64_t>(1, (int64_t)(kDeepBudget / ((size_t)n * 24))));
-  G = std::max<int64_t>(1, std::min<int64_t>(G, INT32_MAX / n));
-  DevBuf kin, kout, vin, vout, offs, temp;
-  CHECK(kin.ensure((size_t)G * n * 8));
-  CHECK(kout.ensure((size_t)G * n * 8));
-  CHECK(vin.ensure((size_t)G * n * 4));
-  CHECK(vout.ensure((size_t)G * n * 4));
-  CHECK(offs.ensure((size_t)(G + 1) * 4));
-  CHECK(ix->w_qnorm.ensure((size_t)G * 8));
-  for (int g0 = 0; g0 < m; g0 += (int)G) {
-    const int gm = (int)std::min<int64_t>(G, m - g0);
-    const float* qg = qc + (int64_t)g0 * ix->dim;
-    hipLaunchKernelGGL(query_norms_kernel, dim3((gm + 3) / 4), dim3(256), 0, st, qg, gm, ix->dim,
-                       ix->w_qnorm.as<double>());
-    const dim3 grid((unsigned)((n + 3) / 4), (unsigned)gm);
-    const uint32_t* mb = ix->has_mask ? ix->maskbits.as<const uint32_t>() : nullptr;
-#define DEEPK(TS)                                                                                  \
-    hipLaunchKernelGGL((deep_keys_kernel<TS>), grid, dim3(256), 0, st, qg, ix->dim,                \
-                       ix->w_qnorm.as<const double>(), ix->rows.as<const TS>(), ix->ld, n,        \
-                       ix->norm64.as<const double>(), mb, kin.as<uint64_t>(), vin.as<uint32_t>())
-    if (ix->dtype == HCR_F16) DEEPK(_Float16); else if (ix->dtype == HCR_BF16) DEEPK(__bf16); else DEEPK(float);
-#undef DEEPK
-    hipLaunchKernelGGL(seg_offsets_kernel, dim3((gm + 256) / 256), dim3(256), 0, st, offs.as<int>(), gm, (int)n);
-    HIPC(hipGetLastError());
-    CHECK(hcr_seg_sort_u64_u32(temp, kin.as<const uint64_t>(), kout.as<uint64_t>(), vin.as<const uint32_t>(),
-                               vout.as<uint32_t>(), (int)(gm * n), gm, offs.as<const int>(), 1, st));
-    const unsigned bx = (unsigned)std::min<int64_t>(1024, (k + 255) / 256);
-    hipLaunchKernelGGL(deep_out_kernel, dim3(bx, (unsigned)gm), dim3(256), 0, st, kout.as<const uint64_t>(),
-                       vout.as<const uint32_t>(), n, k, mode, thr, ix->id_offset,
-                       ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, os + (int64_t)g0 * k,
-                       oi + (int64_t)g0 * k);
-    HIPC(hipGetLastError());
-  }
-  HIPC(hipStreamSynchronize(st));        // (the group buffers are freed on return)
-  return HCR_OK;
+  if (ix->n > INT32_MAX) return set_err(HCR_EINVAL, "k > %d needs an index of < 2^31 rows", kMaxK);
+  int64_t cap = 16384;
+  while (cap < 4 * (int64_t)k && cap < ((int64_t)1 << 30)) cap <<= 1;
+  // (no more slots than rows: an index of n <= cap rows never overflows)
+  int64_t capn = 2;
+  while (capn < ix->n) capn <<= 1;
+  cap = std::max<int64_t>(std::min(cap, capn), kFallbackCap * 2);
+  std::vector<int> all(m);
+  for (int i = 0; i < m; ++i) all[i] = i;
+  return exact_fallback(ix, qc, all, std::vector<uint64_t>(m, 0ull), k, mode, thr, os, oi, st, cap);
 }
 
 // Full search of nq device queries: certified top-k (K1-K4), certificate widening, and the
@@ -1866,74 +1853,8 @@ extern "C" int hcr_score_all(hcr_index* ix, const float* queries, int64_t nq, in
   return HCR_OK;
 }
 
-// ---- sort-based shard merge (g x k > 8192 keys per query: deeper than K5's LDS sort) ----
-// Two stable segmented radix sorts per query over its g x k entries: by id ascending, then by
-// exact score descending -- (score desc, id asc), the tie rule of K5 -- then the first k.
-__global__ void mrg_id_keys_kernel(const int64_t* __restrict__ ids, int g, int64_t nq, int64_t q0, int nqc,
-                                   int k, uint64_t* __restrict__ keys, uint32_t* __restrict__ pos) {
-  const int64_t gk = (int64_t)g * k;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nqc * gk) return;
-  const int64_t q = i / gk, p = i - q * gk, j = p / k, c = p - j * k;
-  keys[i] = (uint64_t)(ids[(j * nq + q0 + q) * k + c] + 1);    // -1 (empty) -> 0
-  pos[i] = (uint32_t)p;
-}
-__global__ void mrg_score_keys_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g,
-                                      int64_t nq, int64_t q0, int nqc, int k, const uint32_t* __restrict__ pos,
-                                      uint64_t* __restrict__ keys) {
-  const int64_t gk = (int64_t)g * k;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nqc * gk) return;
-  const int64_t q = i / gk, p = pos[i], j = p / k, c = p - j * k;
-  const int64_t off = (j * nq + q0 + q) * k + c;
-  keys[i] = ids[off] >= 0 ? ord64(s[off]) : 0ull;
-}
-__global__ void mrg_out_kernel(const double* __restrict__ s, const int64_t* __restrict__ ids, int g, int64_t nq,
-                               int64_t q0, int nqc, int k, const uint32_t* __restrict__ pos,
-                               double* __restrict__ out_s, int64_t* __restrict__ out_i) {
-  const int64_t gk = (int64_t)g * k;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)nqc * k) return;
-  const int64_t q = i / k, t = i - q * k, p = pos[q * gk + t], j = p / k, c = p - j * k;
-  const int64_t off = (j * nq + q0 + q) * k + c;
-  const bool ok = ids[off] >= 0;
-  out_s[(q0 + q) * k + t] = ok ? s[off] : -INFINITY;
-  out_i[(q0 + q) * k + t] = ok ? ids[off] : -1;
-}
-static int merge_sorted(const double* d_scores, const int64_t* d_ids, int g, int64_t nq, int k,
-                        double* d_out_scores, int64_t* d_out_ids, hipStream_t st) {
-  const int64_t gk = (int64_t)g * k;
-  if (gk > INT32_MAX) return set_err(HCR_EINVAL, "g*k must be < 2^31");
-  const int64_t nqc_max = std::max<int64_t>(1, std::min<int64_t>(nq, std::min<int64_t>(INT32_MAX / gk,
-                                                                   (int64_t)(kDeepBudget / (size_t)(gk * 24)))));
-  DevBuf k1, k2, p1, p2, offs, temp;
-  CHECK(k1.ensure((size_t)(nqc_max * gk) * 8));
-  CHECK(k2.ensure((size_t)(nqc_max * gk) * 8));
-  CHECK(p1.ensure((size_t)(nqc_max * gk) * 4));
-  CHECK(p2.ensure((size_t)(nqc_max * gk) * 4));
-  CHECK(offs.ensure((size_t)(nqc_max + 1) * 4));
-  for (int64_t q0 = 0; q0 < nq; q0 += nqc_max) {
-    const int nqc = (int)std::min<int64_t>(nqc_max, nq - q0);
-    const int items = (int)(nqc * gk);
-    const unsigned gr = (unsigned)((items + 255) / 256);
-    hipLaunchKernelGGL(mrg_id_keys_kernel, dim3(gr), dim3(256), 0, st, d_ids, g, nq, q0, nqc, k,
-                       k1.as<uint64_t>(), p1.as<uint32_t>());
-    hipLaunchKernelGGL(seg_offsets_kernel, dim3((nqc + 256) / 256), dim3(256), 0, st, offs.as<int>(), nqc, (int)gk);
-    HIPC(hipGetLastError());
-    CHECK(hcr_seg_sort_u64_u32(temp, k1.as<const uint64_t>(), k2.as<uint64_t>(), p1.as<const uint32_t>(),
-                               p2.as<uint32_t>(), items, nqc, offs.as<const int>(), 0, st));
-    hipLaunchKernelGGL(mrg_score_keys_kernel, dim3(gr), dim3(256), 0, st, d_scores, d_ids, g, nq, q0, nqc, k,
-                       p2.as<const uint32_t>(), k1.as<uint64_t>());
-    HIPC(hipGetLastError());
-    CHECK(hcr_seg_sort_u64_u32(temp, k1.as<const uint64_t>(), k2.as<uint64_t>(), p2.as<const uint32_t>(),
-                               p1.as<uint32_t>(), items, nqc, offs.as<const int>(), 1, st));
-    hipLaunchKernelGGL(mrg_out_kernel, dim3((unsigned)(((int64_t)nqc * k + 255) / 256)), dim3(256), 0, st,
-                       d_scores, d_ids, g, nq, q0, nqc, k, p1.as<const uint32_t>(), d_out_scores, d_out_ids);
-    HIPC(hipGetLastError());
-  }
-  HIPC(hipStreamSynchronize(st));        // (the scratch buffers are freed on return)
-  return HCR_OK;
-}
+// ---- shard merges deeper than K5's 8192 LDS keys (g x k per query): hcr_merge_sorted,
+// deep_sort.hip (one bitonic sort of (score, ~id) keys per query, the first k) ----
 
 extern "C" int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g,
                                      int64_t nq, int k, double* d_out_scores, int64_t* d_out_ids,
@@ -1942,7 +1863,7 @@ extern "C" int hcr_merge_topk_device(const double* d_scores, const int64_t* d_id
   if (nq == 0) return HCR_OK;
   if (!d_scores || !d_ids || !d_out_scores || !d_out_ids) return set_err(HCR_EINVAL, "NULL buffer");
   if ((int64_t)g * k > 8192)
-    return merge_sorted(d_scores, d_ids, g, nq, k, d_out_scores, d_out_ids, (hipStream_t)stream);
+    return hcr_merge_sorted(d_scores, d_ids, g, nq, k, d_out_scores, d_out_ids, (hipStream_t)stream);
   const int M = next_pow2(g * k);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(merge_shards_kernel, dim3((unsigned)nq), dim3(256), (size_t)M * 16, st,

@@ -1341,36 +1341,6 @@ exact_all_kernel(const float* __restrict__ q32, int dim, const double* __restric
   }
 }
 
-// Deep top-k (k > 2048, hcrag_index.hip deep_topk): every row's exact key for a group of
-// queries -- ord64 of the fp64 cosine in K4's summation order (the same scores bit for bit),
-// 0 for rows outside the row mask -- and its row, to be sorted per query (deep_sort.hip).
-template <typename TS>
-__global__ void __launch_bounds__(256)
-deep_keys_kernel(const float* __restrict__ q32, int dim, const double* __restrict__ qnorm,
-                 const TS* __restrict__ rows, int ld, int64_t n, const double* __restrict__ norm64,
-                 const uint32_t* __restrict__ maskbits, uint64_t* __restrict__ keys,
-                 uint32_t* __restrict__ vals) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int q = blockIdx.y;
-  if (row >= n) return;
-  const bool live = !maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u);
-  double acc = 0.0;
-  if (live) {
-    const float* qs = q32 + (int64_t)q * dim;
-    const TS* e = rows + row * ld;
-    for (int d0 = lane * 8; d0 < dim; d0 += 512) {
-      float x[8];
-      load8_f32(e + d0, x);
-      acc8_f64(acc, qs, d0, dim, x);
-    }
-    acc = wave_sum_f64(acc);
-  }
-  if (lane == 0) {
-    keys[(int64_t)q * n + row] = live ? ord64(acc / (qnorm[q] * norm64[row])) : 0ull;
-    vals[(int64_t)q * n + row] = (uint32_t)row;
-  }
-}
 
 // -------------------------------------------------------------------------------------
 // K5: merge g shards' top-k lists ([g][nq][k], exact fp64 scores, -1 = empty).
