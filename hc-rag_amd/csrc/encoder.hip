@@ -25,7 +25,6 @@
 
 #include "encoder_kernels.h"
 #include "gemm_v4.h"
-#include "gemm_split4.h"
 #define HCR_TOPK_TEMPLATES_ONLY   // (gemm_ws.h reaches topk_kernels.h: its kernels live in hcrag_index.hip)
 #include "gemm_ws.h"
 #include "hcrag.h"
@@ -50,12 +49,20 @@ struct EncWork {
                                           // ticket counter per tile (zeroed once, reset by use)
   hipStream_t st = nullptr;               // (split sub-batches only; the first runs unsplit
   hipEvent_t done = nullptr;              //  batches on the caller's stream)
+  bool whole_tiles = false;               // split GEMM in whole-tile rounds only: set when the
+                                          // other sub-batch's stream fills the partly filled
+                                          // last rounds (reference-precision mode, r06)
   void release() {
     DevBuf* b[] = {&x, &xh, &qkv, &ctx, &inter, &y, &pk_off, &pk_map, &pk_ok, &pk_tot, &split_ws, &split_cnt};
     for (DevBuf* d : b) d->release();
   }
 };
 static constexpr int kEncSplits = 2;
+// reference-precision default (HCRAG_ENC_STREAMS overrides): two sub-batches on two streams with
+// whole-tile GEMM rounds, each stream's partly filled last rounds filled by the other's
+// workgroups instead of K-split -- r06 A/B with DM 4: 13.83 -> 13.06 ms per 1024 x 32 batch
+// (r04a measured the split slower, before the K-split remainder and with it on)
+static constexpr int kF32Streams = 2;
 static constexpr int64_t kEncSplitMinSeqs = 128;   // smaller batches run on one stream
 
 struct hcr_encoder {
@@ -84,7 +91,7 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // HCRAG_SPLIT_NONE=1: the split GEMM in whole-tile rounds only (no K-split of the last round;
 // A/B and bit-identity tests of the other paths).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
-// HCRAG_SPLIT_DM=0..4, 10 (one wave per SIMD, gemm_split4.h; 8, 9: diagnostic, wrong results): the split GEMM's LDS-DMA issue placement (gemm_split_kernel's DM; A/B).
+// HCRAG_SPLIT_DM=0|4: the split GEMM's stage pipeline (gemm_split_kernel's DM; A/B; default 4).
 // HCRAG_LN_WITHX=1: the reference-precision LayerNorms also write the fp32 residual stream x
 // (r06 default: only the split activations xh, from which the O / FFN2 epilogues read the
 // residual as h + l 2^-11 -- one 4-byte-per-element write less per LayerNorm; the last layer's
@@ -383,7 +390,7 @@ static int launch_gemm(const TM* W, const TM* X, int K, int N, int T, const floa
 // first and measured neutral to negative (r04n/r04o): its split ranges put the
 // workgroups that share a token tile's activations at different K offsets.
 struct SplitPlan { int ft, nft, full, rem, nsplit; };
-static constexpr int kSplitDM = 0;     // gemm_split_kernel's default DMA issue placement
+static constexpr int kSplitDM = 4;     // gemm_split_kernel's default stage pipeline (r06 A/B)
 static SplitPlan split_plan(int N, int K, int T, int ncu, bool can192, int force_ft, bool split_on) {
   const int ntt = (int)(rup(T, G4_T) / G4_T);
   const int nsteps = K / V3_BK;
@@ -423,7 +430,7 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
   if (N % 8) return hcr_set_errorf(HCR_EINVAL, "internal: GEMM N=%d not a multiple of 8", N);
   // (FFN1's epilogue stages 64-feature halves: 256-feature tiles only)
   constexpr bool can192 = EPI != EPI_BIAS_GELU_SPLIT;
-  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, !enc_hooks().no_split);
+  const SplitPlan p = split_plan(N, K, T, ncu, can192, enc_hooks().gemm_ft, !enc_hooks().no_split && !w.whole_tiles);
   float* ws = nullptr;
   uint32_t* cnt = nullptr;
   if (p.nsplit) {
@@ -439,23 +446,12 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
                      W, X, K, N, T, p.nft, bias, resid, out_h, out_f, ldo, oscale, p.full, p.nsplit, ws, cnt)
 #define HCR_SPLIT(FT_, LIB_, SP_, GRID_)                                                            \
   do {                                                                                              \
-    if (dm == 1) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 1);                                            \
-    else if (dm == 3) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 3);                                       \
-    else if (dm == 4) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 4);                                       \
-    else if (dm == 8) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 8);                                       \
-    else if (dm == 9) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 9);                                       \
-    else if (dm == 2) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 2);                                       \
+    if (dm == 4) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 4);                                            \
     else HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 0);                                                    \
   } while (0)
 #define HCR_SPLIT_FT(FT_, LIB_)                                                                     \
   do {                                                                                              \
-    if (p.full > 0) {                                                                               \
-      if (dm == 10 && FT_ == G4_T)                                                                  \
-        hipLaunchKernelGGL((gemm_split4_kernel<EPI, LIB_>), dim3((unsigned)p.full), dim3(256), 0, st, W, X, K, N, T, \
-                           p.nft, bias, resid, out_h, out_f, ldo, oscale);                          \
-      else                                                                                          \
-        HCR_SPLIT(FT_, LIB_, false, p.full);                                                        \
-    }                                                                                               \
+    if (p.full > 0) HCR_SPLIT(FT_, LIB_, false, p.full);                                            \
     if (p.nsplit > 0) HCR_SPLIT(FT_, LIB_, true, p.rem * p.nsplit);                                 \
   } while (0)
   if constexpr (!can192) {
@@ -703,8 +699,9 @@ extern "C" int hcr_encode_device(hcr_encoder* e, const int32_t* d_ids, const int
   // r04a A/B (bge-base, 1024 x S = 32 ragged, one box): f16 142.3k -> 149.7-152.0k embeddings/s
   // with the split, the f32 mode 66.2k -> 63.9k (its split GEMMs hold 128 KiB of LDS per
   // workgroup and thrash each other's weights): split by default in the fast modes only
-  const int want = enc_hooks().streams > 0 ? enc_hooks().streams : (e->dtype == HCR_F32 ? 1 : kEncSplits);
+  const int want = enc_hooks().streams > 0 ? enc_hooks().streams : (e->dtype == HCR_F32 ? kF32Streams : kEncSplits);
   const int splits = (want <= 1 || n < kEncSplitMinSeqs) ? 1 : kEncSplits;
+  for (EncWork& w : e->work) w.whole_tiles = splits > 1 && e->dtype == HCR_F32;
   if (splits == 1) return run(e->work[0], 0, n, st);
   // Sub-batches of n / splits sequences, each on a stream of its own (ordered after the caller's
   // work through ev_in; the caller's stream waits for every sub-batch's `done` event): every

@@ -581,14 +581,18 @@ __device__ __forceinline__ void ffn1_split_epilogue(char* hs, int lane, const fl
 // (A&S 7.1.26, |error| <= 1.5e-7 + the rcp / exp2 approximations, ~12 instructions).
 // SPLIT = false: one whole tile per workgroup (tile = the workgroup's XCD-remapped index);
 // SPLIT = true: workgroup g is chunk g % nsplit of tile tile_base + g / nsplit (see above).
-// DM: where the stage's LDS-DMA pieces of stage s + 1 are issued inside stage s.  0: spread over
-// the three products (after the 1st, the 2nd and the 3rd); 1: all right after the stage barrier;
-// 2: one after each row block of the first product (Xl'.Wh), so that every piece has the 2nd and
-// 3rd products' MFMA time to land before the next stage's vmcnt(0); 3: TWO stages in flight --
-// after the stage barrier every wave reads the whole stage into registers (24 fragments), a
-// second barrier frees the slot, and the stage after next is issued into it (interleaved with the
-// first product's MFMAs); the next stage's pieces stay in flight across the whole stage (r06:
-// DM 0-2 tied at ~0.5 MFMA busy with 0.35-0.44 of the wave cycles parked at vmcnt / barrier).
+// DM: the stage pipeline.  0: one stage in flight -- a single barrier per stage, the pieces of
+// stage s + 1 issued in three groups after the three products of stage s, vmcnt(0) at the next
+// stage's top.  4 (the default, r06): two stages in flight -- after the stage barrier every wave
+// reads the whole stage into registers (24 fragments), a second barrier frees the slot, and the
+// pieces of the stage after next are spread evenly over all 3 MT NQ MFMAs of the stage (one per
+// ~12), so the CU's vector-memory path sees an even demand.  r06 A/B (profiles/r06/, bge-base
+// f32 encoder, 1024 x 32 ragged): DM 4 -1.2 % against DM 0; the placements tried in between --
+// all pieces right after the barrier, all inside the first product, DM 4's structure with them
+// inside the first product -- tied with DM 0, and without any stage DMA (a diagnostic with stale
+// operands) the encoder ran only 11 % faster: the DMA is not what holds the split GEMM at ~0.5
+// MFMA busy; the per-stage fragment reads and barriers of two waves per SIMD in lockstep are.
+// A one-wave-per-SIMD form (4 waves of 128 x 128, 256 AGPR accumulators) measured 9 % slower.
 template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false, int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
@@ -667,7 +671,7 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
   };
 #pragma unroll
   for (int i = 0; i < PPW; ++i) issue_piece(ks0, i);
-  if constexpr (DM >= 3 && DM != 9) {
+  if constexpr (DM == 4) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) issue_piece(ks0 + 1, i);
   }
@@ -682,50 +686,7 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // DM 8 / 9: DIAGNOSTIC ONLY (wrong results; HCRAG_SPLIT_DM, tools/enc_prof.py timing): DM 4's
-  // loop without the LDS fragment reads after the first stage (8) or without the stage DMA (9)
-  V d_av[MT], d_aw[MT], d_bq[NQ], d_bl[NQ];
-  if constexpr (DM == 8) {
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
-    v3_barrier();
-    g5_read_stage<MT>(lds_addr(ring + WH + offA), lds_addr(ring + WL + offA), lds_addr(ring + XH + offB),
-                      lds_addr(ring + XL + offB), d_av, d_aw, d_bq, d_bl);
-  }
   for (int s = ks0; s < ks1; ++s) {
-    if constexpr (DM == 8 || DM == 9) {
-      if constexpr (DM == 8) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
-      v3_barrier();
-      V av[MT], aw[MT], bq[NQ], bl[NQ];
-      if constexpr (DM == 9) {
-        const char* st = ring + (s & 1) * STAGE;
-        g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
-                          lds_addr(st + XL + offB), av, aw, bq, bl);
-      } else {
-#pragma unroll
-        for (int m = 0; m < MT; ++m) { av[m] = d_av[m]; aw[m] = d_aw[m]; }
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) { bq[n] = d_bq[n]; bl[n] = d_bl[n]; }
-#pragma unroll
-        for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(av[m]), "+v"(aw[m]));
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) asm volatile("" : "+v"(bq[n]), "+v"(bl[n]));
-      }
-      v3_barrier();
-      V as[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) as[m] = av[m] * (_Float16)2048.0f;
-      constexpr int NM = 3 * MT * NQ, GAP = NM / PPW;
-#pragma unroll
-      for (int u = 0; u < NM; ++u) {
-        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
-        if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-        else if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
-        else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
-        if constexpr (DM == 8)
-          if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
-      }
-      continue;
-    }
     if constexpr (DM == 4) {
       // DM 3's two stages in flight with the PPW pieces spread evenly over all 3 x MT x NQ
       // MFMAs of the stage (one per ~12): the CU's vector-memory path sees an even demand
@@ -756,47 +717,8 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
       }
       continue;
     }
-    if constexpr (DM == 3) {
-      // stage s landed (the PPW pieces of stage s + 1 stay in flight)
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
-      v3_barrier();
-      const char* st = ring + (s & 1) * STAGE;
-      V av[MT], aw[MT], bq[NQ], bl[NQ];
-      g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
-                        lds_addr(st + XL + offB), av, aw, bq, bl);
-      v3_barrier();               // every wave holds stage s in registers: its slot is free
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-        if (m < PPW) issue_piece(s + 2, m);
-      }
-#pragma unroll
-      for (int i = MT; i < PPW; ++i) issue_piece(s + 2, i);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x008, NQ, 0);
-        if (m < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      if constexpr (PPW > MT) __builtin_amdgcn_sched_group_barrier(0x020, PPW - MT, 0);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
-      continue;
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     v3_barrier();                 // stage s landed everywhere; everyone done with slot s-1
-    if constexpr (DM == 1) {
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) issue_piece(s + 1, i);
-    }
     const char* st = ring + (s & 1) * STAGE;
     V av[MT], bq[NQ], bl[NQ];
     if constexpr (MT == 8) g5_read8(lds_addr(st + WH + offA), av);
@@ -805,28 +727,12 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     g5_read4(lds_addr(st + XH + offB), bq);
     // Xl' . Wh
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-      if constexpr (DM == 2) {
-        if (m < PPW) issue_piece(s + 1, m);
-      }
-    }
-    if constexpr (DM == 2) {
-#pragma unroll
-      for (int i = MT; i < PPW; ++i) issue_piece(s + 1, i);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x008, NQ, 0);
-        if (m < PPW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      if constexpr (PPW > MT) __builtin_amdgcn_sched_group_barrier(0x020, PPW - MT, 0);
-    }
-    if constexpr (DM == 0) {
-      issue_piece(s + 1, 0);
-      issue_piece(s + 1, 1);
-      issue_piece(s + 1, 2);
-    }
+    issue_piece(s + 1, 0);
+    issue_piece(s + 1, 1);
+    issue_piece(s + 1, 2);
     // Xh . (Wh 2^11): the fragments scaled in registers (exact power of two)
 #pragma unroll
     for (int m = 0; m < MT; ++m) av[m] = av[m] * (_Float16)2048.0f;
@@ -834,11 +740,9 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    if constexpr (DM == 0) {
-      issue_piece(s + 1, 3);
-      issue_piece(s + 1, 4);
-      issue_piece(s + 1, 5);
-    }
+    issue_piece(s + 1, 3);
+    issue_piece(s + 1, 4);
+    issue_piece(s + 1, 5);
     // Xh . Wl'
     if constexpr (MT == 8) g5_read8(lds_addr(st + WL + offA), av);
     else g5_read6(lds_addr(st + WL + offA), av);
@@ -846,10 +750,8 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(av[m], bq[n], acc[m][n]);
-    if constexpr (DM == 0) {
-      issue_piece(s + 1, 6);
-      if constexpr (PPW == 8) issue_piece(s + 1, 7);
-    }
+    issue_piece(s + 1, 6);
+    if constexpr (PPW == 8) issue_piece(s + 1, 7);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 

@@ -4,7 +4,8 @@
 out=$1; script=$2; lim=${3:-1200}
 for i in 1 2 3 4 5 6 7 8; do
   timeout $((lim + 900)) /usr/local/graft/bin/gpurun --timeout "$lim" -- bash "$script" > "$out" 2>&1
-  if grep -q "slot(s) on this pod are busy\|has no free box right now" "$out" && ! grep -q "status=ok" "$out"; then
+  # (also "stopped responding while being prepared": the box failed before the command started)
+  if grep -q "slot(s) on this pod are busy\|has no free box right now\|stopped responding while being prepared" "$out" && ! grep -q "status=ok" "$out"; then
     sleep 150
     continue
   fi
