@@ -81,6 +81,8 @@ def parse():
     p.add_argument("--power-seconds", type=float, default=3.0,
                    help="seconds of back-to-back headline steps with board power / clock sampled "
                         "(0: skip)")
+    p.add_argument("--no-leg-power", action="store_true",
+                   help="do not sample board power / clock during the encoder and configs[4] legs")
     p.add_argument("--large-k", default="1000,2048",
                    help="k values of the k > 256 leg (exact fallback) at B = 64 ('' to skip)")
     p.add_argument("--no-configs4", action="store_true",
@@ -681,6 +683,8 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
         dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ps = PowerSampler(dev.index)                 # (power / clock per leg)
+    if a.no_leg_power:
+        ps.dir = None
     ps.start()
     t0 = time.perf_counter()
     ev0.record()

@@ -201,8 +201,11 @@ __device__ __forceinline__ void lds_bitonic(uint64_t* hi, uint64_t* lo, int M, i
 }
 
 // One block per (chunk, segment): load M keys into LDS, run `full` (every size up to
-// size_hi) or the last-size merge only, store back.
-__global__ void __launch_bounds__(256)
+// size_hi) or the last-size merge only, store back.  1024 threads: 4 compare-exchanges per
+// thread and stage at M = 8192 (a stage is a few dependent LDS round trips, and there are only
+// nseg blocks -- 64 at the bench's deep-k point -- to hide them behind each other).
+constexpr int kBitonicThreads = 1024;
+__global__ void __launch_bounds__(kBitonicThreads)
 bitonic_lds_kernel(uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, int P, int M, int size_hi, int full) {
   extern __shared__ __attribute__((aligned(16))) uint64_t sm_bit[];
   uint64_t* sh = sm_bit;
@@ -241,7 +244,7 @@ int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStre
   if (!attr) return hcr_set_error(HCR_EHIP, "bitonic_lds_kernel: LDS attribute");
   const int M = P < kSortChunk ? P : kSortChunk;
   const size_t lds = (size_t)2 * M * 8;
-  hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(256), lds, st, hi, lo, P, M,
+  hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(kBitonicThreads), lds, st, hi, lo, P, M,
                      M, 1);
   HIPC(hipGetLastError());
   for (int size = 2 * M; size <= P; size <<= 1) {
@@ -250,7 +253,7 @@ int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStre
                          st, hi, lo, P, size, d);
       HIPC(hipGetLastError());
     }
-    hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(256), lds, st, hi, lo, P,
+    hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(kBitonicThreads), lds, st, hi, lo, P,
                        M, size, 0);
     HIPC(hipGetLastError());
   }

@@ -592,7 +592,10 @@ __device__ __forceinline__ void ffn1_split_epilogue(char* hs, int lane, const fl
 // inside the first product -- tied with DM 0, and without any stage DMA (a diagnostic with stale
 // operands) the encoder ran only 11 % faster: the DMA is not what holds the split GEMM at ~0.5
 // MFMA busy; the per-stage fragment reads and barriers of two waves per SIMD in lockstep are.
-// A one-wave-per-SIMD form (4 waves of 128 x 128, 256 AGPR accumulators) measured 9 % slower.
+// A one-wave-per-SIMD form (4 waves of 128 x 128, 256 AGPR accumulators) measured 9 % slower;
+// a staggered DM 4 (waves 4-7 deferring each stage's third product past the next barrier, so the
+// two waves of a SIMD are not in their read phase together) needs the deferred fragments beside
+// DM 4's registers: 832 B/lane of scratch, 36x slower (profiles/r06/r06g) -- not kept.
 template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false, int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
@@ -675,16 +678,6 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
 #pragma unroll
     for (int i = 0; i < PPW; ++i) issue_piece(ks0 + 1, i);
   }
-  // DM 5 / 6 (staggered DM 4): waves 4-7 -- the second wave of every SIMD -- run each stage's
-  // third product (Xh . Wl') after the NEXT stage's first barrier, beside waves 0-3's fragment
-  // reads, so that the two waves of a SIMD are not in their read phase at the same time
-  // (MI355X_MICROARCH.md 'two waves per SIMD' item 9); the fragments it needs (Wl', Xh) stay in
-  // registers across the barrier.  DM 6: waves 4-7 also at s_setprio 1 (item 4).
-  const bool late = (DM == 5 || DM == 6) && wave >= 4;
-  if constexpr (DM == 6) {
-    if (late) __builtin_amdgcn_s_setprio(1);
-  }
-
   const int fr = lane & 15, fc = lane >> 4;
   const int fslot = v3_slot(fc, fr);
   const int offA = (wm * (FT / 2) + fr) * 64 + fslot * 16;
@@ -695,61 +688,7 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
 #pragma unroll
     for (int n = 0; n < NQ; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // one stage of the staggered pipeline; LATE: waves 4-7 (the deferred third product of the
-  // previous stage first, this stage's third product kept for the next)
-  V aw5[MT], bq5[NQ];
-  auto stage5 = [&](int s, auto late_c) __attribute__((always_inline)) {
-    constexpr bool LATE = decltype(late_c)::value;
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
-    v3_barrier();
-    if constexpr (LATE) {
-      if (s > ks0) {
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(aw5[m], bq5[n], acc[m][n]);
-      }
-    }
-    const char* st = ring + (s & 1) * STAGE;
-    V av[MT], bl[NQ];
-    g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
-                      lds_addr(st + XL + offB), av, aw5, bq5, bl);
-    v3_barrier();
-    // (Wh scaled by 2^11 in place after the first product: DM 4's separate copy costs the
-    // registers the deferred fragments need)
-    constexpr int NM = (LATE ? 2 : 3) * MT * NQ, GAP = NM / PPW;
-#pragma unroll
-    for (int u = 0; u < NM; ++u) {
-      const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
-      if (u == MT * NQ) {
-#pragma unroll
-        for (int mm = 0; mm < MT; ++mm) av[mm] = av[mm] * (_Float16)2048.0f;
-      }
-      if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-      else if (prod == 1) acc[m][n] = Op::run(av[m], bq5[n], acc[m][n]);
-      else acc[m][n] = Op::run(aw5[m], bq5[n], acc[m][n]);
-      if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
-    }
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, GAP, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    }
-  };
-  if constexpr (DM == 5 || DM == 6) {
-    if (late) {
-      for (int s = ks0; s < ks1; ++s) stage5(s, std::true_type{});
-      if (ks1 > ks0) {            // the last stage's deferred third product
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-          for (int n = 0; n < NQ; ++n) acc[m][n] = Op::run(aw5[m], bq5[n], acc[m][n]);
-      }
-    } else {
-      for (int s = ks0; s < ks1; ++s) stage5(s, std::false_type{});
-    }
-  }
-  for (int s = ks0; s < ks1 && (DM != 5 && DM != 6); ++s) {
+  for (int s = ks0; s < ks1; ++s) {
     if constexpr (DM == 4) {
       // DM 3's two stages in flight with the PPW pieces spread evenly over all 3 x MT x NQ
       // MFMAs of the stage (one per ~12): the CU's vector-memory path sees an even demand
@@ -772,6 +711,44 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
         else if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
         else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
         if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
+      }
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, GAP, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      continue;
+    }
+    if constexpr (DM == 7 || DM == 8) {
+      // DM 4 with the slot-freeing barrier moved into the MFMA phase -- after the first (DM 7)
+      // or second (DM 8) product: a wave starts its MFMAs as soon as its own fragments landed,
+      // beside the other waves' reads, instead of every wave waiting for the slowest read; the
+      // stage-after-next pieces are spread over the products after the barrier
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
+      v3_barrier();
+      const char* st = ring + (s & 1) * STAGE;
+      V av[MT], aw[MT], bq[NQ], bl[NQ];
+      g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
+                        lds_addr(st + XL + offB), av, aw, bq, bl);
+      constexpr int NB = (DM == 7 ? 1 : 2) * MT * NQ;          // MFMAs before the barrier
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
+        if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
+        else acc[m][n] = Op::run(av[m] * (_Float16)2048.0f, bq[n], acc[m][n]);
+      }
+      v3_barrier();
+      V as[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) as[m] = av[m] * (_Float16)2048.0f;
+      constexpr int NA = 3 * MT * NQ - NB, GAP = NA / PPW;
+#pragma unroll
+      for (int u = NB; u < 3 * MT * NQ; ++u) {
+        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
+        if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
+        else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
+        const int v = u - NB;
+        if (v % GAP == GAP - 1 && v / GAP < PPW) issue_piece(s + 2, v / GAP);
       }
 #pragma unroll
       for (int i = 0; i < PPW; ++i) {
@@ -817,9 +794,6 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
     if constexpr (PPW == 8) issue_piece(s + 1, 7);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (DM == 6) {
-    if (late) __builtin_amdgcn_s_setprio(0);
-  }
 
   if constexpr (SPLIT) {
     const int slot = tile - tile_base;

@@ -1047,6 +1047,14 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
 constexpr int kFbHistBins = 512;
 constexpr int kFbGroupsPerScan = 4;  // query groups of kFbGroup per MFMA-prefiltered scan
 constexpr float kFbHistRange = 1.0625f;
+constexpr int kPairBatch = 4;                 // K6m: admitted pairs rescored together
+constexpr int kPairQueue = kPairBatch - 1 + 4 * 64 + 1;   // per-wave queue slots
+
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <typename TS, int KS, bool HIST>
 __global__ void __launch_bounds__(256)
@@ -1065,8 +1073,11 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   using V = typename Op::V;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
   constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
-  __shared__ __attribute__((aligned(16))) char sm[HB > FB ? HB : FB];
-  __shared__ double s_tc[kFbGroup];
+  constexpr size_t FBQ = FB + (size_t)4 * kPairQueue * 8;            // + the pair queues
+  static_assert(FB % 8 == 0, "pair queue alignment");
+  __shared__ __attribute__((aligned(16))) char sm[HB > FBQ ? HB : FBQ];
+  __shared__ double s_tc[kFbGroup], s_qn[kFbGroup], s_hlo[kFbGroup], s_hhi[kFbGroup];
+  __shared__ uint64_t s_thh[kFbGroup], s_thl[kFbGroup];
   unsigned int* s_hist = reinterpret_cast<unsigned int*>(sm);                        // HIST
   unsigned int (*s_cnt)[kFbBins + 1] = reinterpret_cast<unsigned int (*)[kFbBins + 1]>(sm);
   unsigned long long (*s_min)[kFbBins + 1] =
@@ -1089,6 +1100,13 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       const int q = threadIdx.x;
       // the prefilter bound: pairs below it cannot reach the threshold key's score
       s_tc[q] = (q < nqg && active[qg0 + q]) ? unord64(th_hi[qg0 + q]) - eps[qg0 + q] : INFINITY;
+      if (q < nqg) {              // (the admission test's per-query values, read per pair)
+        s_qn[q] = qnorm[qg0 + q];
+        s_thh[q] = th_hi[qg0 + q];
+        s_thl[q] = th_lo[qg0 + q];
+        s_hlo[q] = h_lo[qg0 + q];
+        s_hhi[q] = h_hi[qg0 + q];
+      }
     }
   }
   __syncthreads();
@@ -1104,6 +1122,67 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   }
   const bool qok = ql < nqg && active[qg0 + ql];
   const double tcq = HIST ? 0.0 : s_tc[ql];
+  // K6m's admitted (row, query) pairs: a queue per wave in the LDS above the histograms (at
+  // most kPairBatch - 1 left over + 4 x 64 per tile); entry = row << 8 | group-local query
+  uint64_t* pq = reinterpret_cast<uint64_t*>(sm + FB) + wave * kPairQueue;
+  int qn = 0;
+  // the exact fp64 cosine of np (<= kPairBatch) queued pairs at once: every lane's 8-wide
+  // pieces of all the pairs' rows are loaded together (one memory round trip instead of one per
+  // pair), each pair in K6's summation order (so bit-identical to K4 / K6); lane p then runs
+  // pair p's key test, append and histogram
+  auto rescore_batch = [&](const uint64_t* e, int np) __attribute__((always_inline)) {
+    int64_t prow[kPairBatch];
+    int pqs[kPairBatch];
+#pragma unroll
+    for (int p = 0; p < kPairBatch; ++p) {
+      const uint64_t v = e[p < np ? p : 0];
+      prow[p] = (int64_t)(v >> 8);
+      pqs[p] = (int)(v & 255u);
+    }
+    int64_t my_row = prow[0];
+    int my_q = pqs[0];
+#pragma unroll
+    for (int p = 1; p < kPairBatch; ++p)
+      if (lane == p) { my_row = prow[p]; my_q = pqs[p]; }
+    const double nr = lane < np ? norm64[my_row] : 1.0;
+    double ex[kPairBatch];
+#pragma unroll
+    for (int p = 0; p < kPairBatch; ++p) ex[p] = 0.0;
+    for (int d0 = lane * 8; d0 < dim; d0 += 512) {
+      float x[kPairBatch][8];
+#pragma unroll
+      for (int p = 0; p < kPairBatch; ++p) load8_f32(rows + prow[p] * ld + d0, x[p]);
+#pragma unroll
+      for (int p = 0; p < kPairBatch; ++p) acc8_f64(ex[p], q32 + (int64_t)(qg0 + pqs[p]) * dim, d0, dim, x[p]);
+    }
+    double my_ex = 0.0;
+#pragma unroll
+    for (int p = 0; p < kPairBatch; ++p) {
+      const double t = wave_sum_f64(ex[p]);
+      if (lane == p) my_ex = t;
+    }
+    if (lane < np) {
+      const int q = qg0 + my_q;
+      const double sc = my_ex / (s_qn[my_q] * nr);
+      const uint64_t h = ord64(sc);
+      const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)my_row);
+      if (h > s_thh[my_q] || (h == s_thh[my_q] && l >= s_thl[my_q])) {
+        const unsigned int pos = atomicAdd(&cnt[q], 1u);
+        if (pos < (unsigned int)cap) {
+          buf_hi[(size_t)q * cap + pos] = h;
+          buf_lo[(size_t)q * cap + pos] = l;
+        }
+        const double lo = s_hlo[my_q], hi = s_hhi[my_q];
+        int b = kFbBins;
+        if (sc < hi) {
+          const double tt = (sc - lo) * ((double)kFbBins / (hi - lo));
+          b = tt < 0.0 ? 0 : tt >= (double)(kFbBins - 1) ? kFbBins - 1 : (int)tt;
+        }
+        atomicAdd(&s_cnt[my_q][b], 1u);
+        atomicMin(&s_min[my_q][b], (unsigned long long)h);
+      }
+    }
+  };
   const int64_t ntile = (n + 15) / 16;
   const int64_t stride = (int64_t)nchunks * 2;
   // (HIST: runs of 4 tiles out of every 4 hstride -- a sample of the rows when hstride > 1)
@@ -1162,47 +1241,33 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
         atomicAdd(&s_hist[ql * kFbHistBins + b], 1u);
       }
     } else {
+      // admitted pairs go to the wave's queue; full batches of kPairBatch are rescored at once
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        bool adm = rok[r] && (double)(acc[r] * iv[r]) >= tcq;
-        uint64_t m = __builtin_amdgcn_ballot_w64(adm);
-        while (m) {                                  // a wave per admitted pair (rare)
-          const int src = __builtin_ctzll(m);
-          m &= m - 1;
-          const int qs_ = __builtin_amdgcn_readlane(ql, src);    // (group-local)
-          const int q = qg0 + qs_;
-          const int64_t row = rb - (lane >> 4) * 4 + (src >> 4) * 4 + r;
-          const TS* e = rows + row * ld;
-          const float* qs = q32 + (int64_t)q * dim;
-          double ex = 0.0;
-          for (int d0 = lane * 8; d0 < dim; d0 += 512) {
-            float x[8];
-            load8_f32(e + d0, x);
-            acc8_f64(ex, qs, d0, dim, x);
-          }
-          ex = wave_sum_f64(ex);
-          if (lane == 0) {
-            const double sc = ex / (qnorm[q] * norm64[row]);
-            const uint64_t h = ord64(sc);
-            const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)row);
-            if (h > th_hi[q] || (h == th_hi[q] && l >= th_lo[q])) {
-              const unsigned int p = atomicAdd(&cnt[q], 1u);
-              if (p < (unsigned int)cap) {
-                buf_hi[(size_t)q * cap + p] = h;
-                buf_lo[(size_t)q * cap + p] = l;
-              }
-              const double lo = h_lo[q], hi = h_hi[q];
-              int b = kFbBins;
-              if (sc < hi) {
-                const double tt = (sc - lo) * ((double)kFbBins / (hi - lo));
-                b = tt < 0.0 ? 0 : tt >= (double)(kFbBins - 1) ? kFbBins - 1 : (int)tt;
-              }
-              atomicAdd(&s_cnt[qs_][b], 1u);
-              atomicMin(&s_min[qs_][b], (unsigned long long)h);
-            }
-          }
+        const bool adm = rok[r] && (double)(acc[r] * iv[r]) >= tcq;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(adm);
+        if (adm) {
+          const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          pq[qn + below] = ((uint64_t)(rb + r) << 8) | (uint64_t)ql;
         }
+        qn += __builtin_popcountll(m);
       }
+      qn = __builtin_amdgcn_readfirstlane(qn);
+      if (qn >= kPairBatch) {
+        lds_wave_sync();
+        while (qn >= kPairBatch) {
+          qn -= kPairBatch;
+          rescore_batch(pq + qn, kPairBatch);
+        }
+        lds_wave_sync();
+      }
+    }
+  }
+  if constexpr (!HIST) {
+    if (qn > 0) {
+      lds_wave_sync();
+      rescore_batch(pq, qn);
     }
   }
   __syncthreads();

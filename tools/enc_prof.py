@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--seed", type=int, default=77)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--mm", type=int, default=0, help="torch.mm fp16 8192^3 calls after the encoder")
+    ap.add_argument("--power", action="store_true", help="sample board power / clock (bench.PowerSampler) while timing")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = bench.ENC_SHAPES[a.model]
@@ -48,15 +49,20 @@ def main():
         enc.encode_device(ids, mask, out, stream)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ps = bench.PowerSampler(0) if a.power else None
+    if ps:
+        ps.start()
     e0.record()
     for _ in range(a.steps):
         enc.encode_device(ids, mask, out, stream)
     e1.record()
     torch.cuda.synchronize()
+    pc = ps.stop() if ps else None
     ms = e0.elapsed_time(e1) / a.steps
     res = {"model": a.model, "mode": a.mode, "batch": B, "seq": S, "ms_per_batch": round(ms, 3),
            "embeddings_per_s": round(B / ms * 1e3, 1), "tokens_valid": int(mask.sum().item()),
-           "split_dm": os.environ.get("HCRAG_SPLIT_DM", "default")}
+           "split_dm": os.environ.get("HCRAG_SPLIT_DM", "default"),
+           "streams": os.environ.get("HCRAG_ENC_STREAMS", "default"), "power": pc}
     enc.close()
     if a.mm:
         A = torch.randn((8192, 8192), device=dev, dtype=torch.float16)
