@@ -91,7 +91,7 @@ static int64_t rup(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // HCRAG_SPLIT_NONE=1: the split GEMM in whole-tile rounds only (no K-split of the last round;
 // A/B and bit-identity tests of the other paths).
 // HCRAG_ENC_STREAMS=1: one stream per batch (no sub-batch split; A/B of the split).
-// HCRAG_SPLIT_DM=0|4|7|8: the split GEMM's stage pipeline (gemm_split_kernel's DM; A/B; default 4).
+// HCRAG_SPLIT_DM=0|4: the split GEMM's stage pipeline (gemm_split_kernel's DM; A/B; default 4).
 // HCRAG_LN_WITHX=1: the reference-precision LayerNorms also write the fp32 residual stream x
 // (r06 default: only the split activations xh, from which the O / FFN2 epilogues read the
 // residual as h + l 2^-11 -- one 4-byte-per-element write less per LayerNorm; the last layer's
@@ -447,8 +447,6 @@ static int launch_gemm_split(EncWork& w, int ncu, const _Float16* W, const _Floa
 #define HCR_SPLIT(FT_, LIB_, SP_, GRID_)                                                            \
   do {                                                                                              \
     if (dm == 4) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 4);                                            \
-    else if (dm == 7) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 7);                                       \
-    else if (dm == 8) HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 8);                                       \
     else HCR_SPLIT_DM(FT_, LIB_, SP_, GRID_, 0);                                                    \
   } while (0)
 #define HCR_SPLIT_FT(FT_, LIB_)                                                                     \

@@ -595,7 +595,10 @@ __device__ __forceinline__ void ffn1_split_epilogue(char* hs, int lane, const fl
 // A one-wave-per-SIMD form (4 waves of 128 x 128, 256 AGPR accumulators) measured 9 % slower;
 // a staggered DM 4 (waves 4-7 deferring each stage's third product past the next barrier, so the
 // two waves of a SIMD are not in their read phase together) needs the deferred fragments beside
-// DM 4's registers: 832 B/lane of scratch, 36x slower (profiles/r06/r06g) -- not kept.
+// DM 4's registers: 832 B/lane of scratch, 36x slower (profiles/r06/r06g); DM 4 with the
+// slot-freeing barrier moved into the MFMA phase (after the first or second product, so a wave
+// starts its MFMAs as soon as its own fragments land) measured 1.5-2.5 % slower (r06j) -- neither
+// kept.
 template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false, int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
@@ -711,44 +714,6 @@ gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X
         else if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
         else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
         if (u % GAP == GAP - 1 && u / GAP < PPW) issue_piece(s + 2, u / GAP);
-      }
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, GAP, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      continue;
-    }
-    if constexpr (DM == 7 || DM == 8) {
-      // DM 4 with the slot-freeing barrier moved into the MFMA phase -- after the first (DM 7)
-      // or second (DM 8) product: a wave starts its MFMAs as soon as its own fragments landed,
-      // beside the other waves' reads, instead of every wave waiting for the slowest read; the
-      // stage-after-next pieces are spread over the products after the barrier
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PPW) : "memory");
-      v3_barrier();
-      const char* st = ring + (s & 1) * STAGE;
-      V av[MT], aw[MT], bq[NQ], bl[NQ];
-      g5_read_stage<MT>(lds_addr(st + WH + offA), lds_addr(st + WL + offA), lds_addr(st + XH + offB),
-                        lds_addr(st + XL + offB), av, aw, bq, bl);
-      constexpr int NB = (DM == 7 ? 1 : 2) * MT * NQ;          // MFMAs before the barrier
-#pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
-        if (prod == 0) acc[m][n] = Op::run(av[m], bl[n], acc[m][n]);
-        else acc[m][n] = Op::run(av[m] * (_Float16)2048.0f, bq[n], acc[m][n]);
-      }
-      v3_barrier();
-      V as[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) as[m] = av[m] * (_Float16)2048.0f;
-      constexpr int NA = 3 * MT * NQ - NB, GAP = NA / PPW;
-#pragma unroll
-      for (int u = NB; u < 3 * MT * NQ; ++u) {
-        const int prod = u / (MT * NQ), m = (u / NQ) % MT, n = u % NQ;
-        if (prod == 1) acc[m][n] = Op::run(as[m], bq[n], acc[m][n]);
-        else acc[m][n] = Op::run(aw[m], bq[n], acc[m][n]);
-        const int v = u - NB;
-        if (v % GAP == GAP - 1 && v / GAP < PPW) issue_piece(s + 2, v / GAP);
       }
 #pragma unroll
       for (int i = 0; i < PPW; ++i) {

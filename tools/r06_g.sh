@@ -18,4 +18,7 @@ for r in 1 2; do
 done && \
 HCRAG_SPLIT_DM=5 T ${TAG}_kt_dm5 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_kt_dm5 -o run -- python tools/enc_prof.py --steps 5 && \
 HCRAG_SPLIT_DM=5 HCRAG_ENC_STREAMS=1 T ${TAG}_sq_dm5 120 rocprofv3 --pmc $SQ1 --output-format csv -d gpurun_out/${TAG}_sq_dm5 -o run -- python tools/enc_prof.py --steps 3 && \
+BE() { tag=$1; ev=$2; shift 2; timeout -k 10 240 env $ev python -u bench.py "$@" --power-seconds 0 --no-cpu-baseline --no-configs0 --no-configs1 --no-configs4 --pipe-modes '' --sweep '' --large-k '' --no-vendor-gemm --enc-modes f32 --steps 5 --warmup 2 > gpurun_out/${TAG}_be_${tag}.log 2>&1 || exit 99; }
+BE small_s2 HCRAG_SPLIT_DM=4 --rows 200000 && BE small_s1 HCRAG_ENC_STREAMS=1 --rows 200000 && \
+BE big_s2 HCRAG_SPLIT_DM=4 && BE big_s1 HCRAG_ENC_STREAMS=1 && BE big_s2_pow3 HCRAG_SPLIT_DM=4 --power-seconds 3 && \
 echo ALLDONE
