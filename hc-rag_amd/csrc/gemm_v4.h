@@ -602,7 +602,10 @@ __device__ __forceinline__ void ffn1_split_epilogue(char* hs, int lane, const fl
 // accumulators through tied inline-asm MFMAs, the next fragments' reads in flight under the
 // current product, one barrier per stage) ran 13.84 ms against DM 4's 13.1 (r06k): that wave
 // also issues all 16 LDS-DMA pieces of a stage, ~60-185 cycles each (MI355X_MICROARCH.md), with
-// no partner wave to hide them -- none of these kept.
+// no partner wave to hide them; loader waves issuing all the DMA beside compute waves that only
+// read and multiply (256 x 128 tiles, a 3-slot ring: bit-identical, 14.5 ms, r06p) fill at ~26
+// GB/s per CU -- 6.7 TB/s chip-wide, where DM 4 runs at ~5 TB/s of L2 -> LDS fill with a third
+// fewer bytes per flop -- none of these kept.
 template <int EPI, int FT = G4_T, bool LIBERF = false, bool SPLIT = false, int DM = 0>
 __global__ void __launch_bounds__(V3_NT, 1)
 gemm_split_kernel(const _Float16* __restrict__ W, const _Float16* __restrict__ X, int K, int N_real,
