@@ -1358,6 +1358,49 @@ int hcr_merge_sorted(const double* d_scores, const int64_t* d_ids, int g, int64_
                      int64_t* d_out_ids, hipStream_t st);
 static constexpr size_t kDeepBudget = (size_t)2 << 30;   // admission + sort buffers of a deep group
 
+// Round 0's starting thresholds from K6h's coarse histograms, on the device (r06: no readback
+// and host pass between K6h and the first K6m round).  One wave per query without a starting
+// threshold: from the top bin down, the first bin where the count reaches need_rows gives T =
+// (lower edge) - 1e-5 - eps_q (every row counted there has exact >= T); no such
+// bin leaves the query at "every row".  Lane l holds bins 8 l .. 8 l + 7.
+__global__ void __launch_bounds__(64)
+hist_seed_kernel(const unsigned int* __restrict__ hist, const double* __restrict__ eps, int ng,
+                 unsigned long long need_rows, int est_flag, uint64_t* __restrict__ thh,
+                 double* __restrict__ hlo, int* __restrict__ est) {
+  const int q = blockIdx.x, lane = threadIdx.x;
+  if (q >= ng || thh[q] != 0ull || eps[q] < 0.0) return;      // (eps < 0: zero query)
+  static_assert(kFbHistBins == 8 * 64, "8 bins per lane");
+  const unsigned int* h = hist + (size_t)q * kFbHistBins + lane * 8;
+  unsigned long long mine = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mine += h[i];
+  // inclusive suffix sums over the lanes (lane l: bins >= 8 l)
+  unsigned long long suf = mine;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long o = __shfl_down(suf, off);
+    if (lane + off < 64) suf += o;
+  }
+  const uint64_t hit = __builtin_amdgcn_ballot_w64(suf >= need_rows);
+  if (!hit) return;
+  const int L = 63 - __builtin_clzll(hit);                    // the highest lane reaching it
+  if (lane != L) return;
+  unsigned long long acc = suf - mine;                        // bins above this lane's
+  const double bw = 2.0 * kFbHistRange / kFbHistBins;
+  for (int i = 7; i >= 0; --i) {
+    acc += h[i];
+    if (acc >= need_rows) {
+      const int b = lane * 8 + i;
+      // the host's (-R + b bw) - 1e-5 - eps, operation for operation (no contraction)
+      const double T = __dsub_rn(__dsub_rn(__dadd_rn(-(double)kFbHistRange, __dmul_rn((double)b, bw)), 1e-5), eps[q]);
+      thh[q] = ord64(T);
+      hlo[q] = T;
+      est[q] = est_flag;
+      return;
+    }
+  }
+}
+
 static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>& idx,
                           const std::vector<uint64_t>& sk, int k, int mode, double thr, double* os,
                           int64_t* oi, hipStream_t st, int64_t cap64 = kFallbackCap) {
@@ -1487,33 +1530,10 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                                                 : (uint64_t)std::ceil(fk + 5.0 * std::sqrt(fk) + 3.0);
         launch_mfil(ng, true, hstride);
         HIPC(hipGetLastError());
-        std::vector<unsigned int> hist((size_t)ng * kFbHistBins);
-        std::vector<double> epsq(ng);
-        HIPC(hipMemcpyAsync(hist.data(), ix->f_ch.p, hist.size() * 4, hipMemcpyDeviceToHost, st));
-        HIPC(hipMemcpyAsync(epsq.data(), ix->f_eps.p, (size_t)ng * 8, hipMemcpyDeviceToHost, st));
-        HIPC(hipStreamSynchronize(st));
-        const double bw = 2.0 * kFbHistRange / kFbHistBins;
-        for (int i = 0; i < ng; ++i) {
-          if (thh[i] != 0ull || epsq[i] < 0.0) continue;    // (eps < 0: zero query, all scores 0)
-          uint64_t acc = 0;
-          for (int b = kFbHistBins - 1; b >= 0; --b) {
-            acc += hist[(size_t)i * kFbHistBins + b];
-            if (acc >= need_rows) {
-              est[i] = hstride > 1 ? 1 : 0;
-              // >= k rows have c >= edge (less the float binning's rounding), so exact >= T
-              const double T = (-kFbHistRange + b * bw) - 1e-5 - epsq[i];
-              uint64_t u;
-              memcpy(&u, &T, 8);
-              thh[i] = u ^ ((u >> 63) ? 0xFFFFFFFFFFFFFFFFull : 0x8000000000000000ull);   // ord64
-              hlo[i] = T;
-              break;
-            }
-          }
-        }
-        HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-        HIPC(hipMemcpyAsync(ix->f_hlo.p, hlo.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-        HIPC(hipMemcpyAsync(ix->f_est.p, est.data(), (size_t)ng * 4, hipMemcpyHostToDevice, st));
-        HIPC(hipStreamSynchronize(st));     // (the host vectors above are copied from)
+        hipLaunchKernelGGL(hist_seed_kernel, dim3((unsigned)ng), dim3(64), 0, st, ix->f_ch.as<const unsigned int>(),
+                           ix->f_eps.as<const double>(), ng, (unsigned long long)need_rows, hstride > 1 ? 1 : 0,
+                           ix->f_thh.as<uint64_t>(), ix->f_hlo.as<double>(), ix->f_est.as<int>());
+        HIPC(hipGetLastError());
         ix->stats.fallback_rounds += 1;
       }
     }

@@ -1047,10 +1047,10 @@ exact_filter_kernel(const float* __restrict__ q32, int nq, int dim,
 constexpr int kFbHistBins = 512;
 constexpr int kFbGroupsPerScan = 4;  // query groups of kFbGroup per MFMA-prefiltered scan
 constexpr float kFbHistRange = 1.0625f;
-// K6m: admitted pairs rescored together -- 8 at ld = 384 (registers to spare beside 12 query
-// fragments), 4 at 768 / 1024 -- and the per-wave queue slots (a batch's leftover + one tile)
-constexpr int kPairBatchMax = 8;
-constexpr int kPairQueue = kPairBatchMax - 1 + 4 * 64 + 1;
+// K6m: admitted pairs rescored together, and the per-wave queue slots (a batch's leftover + one
+// tile).  (8 at a time at ld = 384 measured the same as 4, r06r: 891.7 vs 900 µs per scan.)
+constexpr int kPairBatch = 4;
+constexpr int kPairQueue = kPairBatch - 1 + 4 * 64 + 1;
 
 __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1073,7 +1073,6 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
                          unsigned int* __restrict__ c_hist, int ngroups, int hstride) {
   using Op = MfmaOp<TS>;
   using V = typename Op::V;
-  constexpr int kPairBatch = KS <= 12 ? kPairBatchMax : 4;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
   constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
   constexpr size_t FBQ = FB + (size_t)4 * kPairQueue * 8;            // + the pair queues
