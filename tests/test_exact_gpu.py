@@ -486,6 +486,31 @@ def test_deep_k_mfma_route_overflow_and_long_sort(hc, dtype):
         assert ix.last_stats()["fallback_rounds"] >= 3      # the overflow took extra rounds
 
 
+@pytest.mark.parametrize("D,dtype", [(768, "f16"), (1024, "bf16")])
+def test_deep_k_mfma_route_wide_rows(hc, D, dtype):
+    """The deep path on the MFMA-prefiltered route at D = 768 / 1024 (K6h / K6m with 24 / 32
+    query fragments, the admission queue rescoring 4 pairs at a time): raw rows, 2 query groups
+    (32 + 3), k = 3000, then a row mask and a threshold at k = 4100 -- ids identical to the fp64
+    oracle, scores to 1e-12."""
+    rng = np.random.default_rng(D + 3)
+    N, B = 24000 + 5, 35
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[1] = E[7]
+    mask = rng.random(N) < 0.75
+    with hc.VectorIndex(D, dtype) as ix:
+        ix.add(E, normalize=False)
+        R = ix.get_rows().astype(np.float64)
+        s, i = ix.search(Q, 3000)
+        es, ei = O.cosine_topk(Q, R, 3000)
+        _check(s, i, es, ei)
+        assert ix.last_stats()["fallback_queries"] == B
+        ix.set_rowmask(mask)
+        s, i = ix.search(Q[:5], 4100, threshold=0.01)
+        es, ei = O.cosine_topk(Q[:5], R, 4100, threshold=0.01, rowmask=mask)
+        _check(s, i, es, ei)
+
+
 def test_deep_k_multi_device_sorted_merge(hc):
     """k = 5000 over a 3-shard multi-device index (shards on one device): each shard's deep
     top-k, then the shard merge by one bitonic sort of (score, ~id) keys (g x k > 8192), against the
