@@ -224,8 +224,9 @@ int hcr_index_test_hook(hcr_index* index, int hook, int value);
 
 /* Merge g row-shards' per-query top-k lists (device, each [g][nq][k] scores fp64 + ids)
  * into the global top-k (score desc, id asc).  Used after the cross-GPU exchange of
- * SURVEY.md §8(e).  Asynchronous on `stream` for g x k <= 8192; deeper merges (two stable
- * segmented sorts per query) synchronise `stream` before returning. */
+ * SURVEY.md §8(e).  Asynchronous on `stream` for g x k <= 8192; deeper merges (one bitonic
+ * sort of the (score, id) keys per query, deep_sort.hip) synchronise `stream` before
+ * returning. */
 int hcr_merge_topk_device(const double* d_scores, const int64_t* d_ids, int g, int64_t nq,
                           int k, double* d_out_scores, int64_t* d_out_ids, void* stream);
 
