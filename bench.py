@@ -623,13 +623,16 @@ def configs4_leg(a, hc, dev, steps=3):
         search()
     step()
     evs.clear()
-    #  the board's power and clock over the timed steps, and the encoder's
-    # own time inside each step from events around it -- not the difference of two loops
-    ps = PowerSampler(dev.index)
-    ps.start()
+    # the encoder's own time inside each step from events around it -- not the difference of
+    # two loops -- and the board's power and clock over as many steps again
     per = timed_steps(step, steps, dev, None)
-    pc = ps.stop()
     enc_in_step = sorted(a.elapsed_time(b) for a, b in evs)
+    ps = PowerSampler(dev.index)                 # (sampled after the timed steps, as above)
+    ps.start()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    pc = ps.stop()
     ix.set_timing(True)
     km = 0.0
     for _ in range(steps):
@@ -682,10 +685,6 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     if dist:
         dist.barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ps = PowerSampler(dev.index)                 # (power / clock per leg)
-    if a.no_leg_power:
-        ps.dir = None
-    ps.start()
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(a.enc_steps):
@@ -693,6 +692,16 @@ def encoder_leg(a, hc, dev, rank, world, dist, mode, B):
     ev1.record()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    #  board power / clock of this leg, sampled over the same number of
+    # batches right after the timed ones: the sysfs reads cost the encoder ~2 % (r06h), so they
+    # stay out of the timed loop
+    ps = PowerSampler(dev.index)
+    if a.no_leg_power:
+        ps.dir = None
+    ps.start()
+    for _ in range(a.enc_steps):
+        enc.encode_device(ids, mask, out, stream)
+    torch.cuda.synchronize()
     pc = ps.stop()
     if dist:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
