@@ -1051,6 +1051,10 @@ constexpr float kFbHistRange = 1.0625f;
 // tile).  (8 at a time at ld = 384 measured the same as 4, r06r: 891.7 vs 900 µs per scan.)
 constexpr int kPairBatch = 4;
 constexpr int kPairQueue = kPairBatch - 1 + 4 * 64 + 1;
+// K6m: admitted keys staged per block in LDS (r06: the returning global atomic per admitted pair
+// was one of two dependent round trips in every rescore batch); one atomic per query and block
+// at the end reserves their slots; past kStage the pairs append to global memory directly
+constexpr int kStage = 384;
 
 __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1075,11 +1079,14 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   using V = typename Op::V;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
   constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
-  constexpr size_t FBQ = FB + (size_t)4 * kPairQueue * 8;            // + the pair queues
+  constexpr size_t FBQ0 = FB + (size_t)4 * kPairQueue * 8;           // + the pair queues
+  constexpr size_t FBQ = FBQ0 + (size_t)kStage * (8 + 4 + 2 + 2);     // + the staged keys
   static_assert(FB % 8 == 0, "pair queue alignment");
+  static_assert(FBQ <= 65536, "K6m LDS");
   __shared__ __attribute__((aligned(16))) char sm[HB > FBQ ? HB : FBQ];
   __shared__ double s_tc[kFbGroup], s_qn[kFbGroup], s_hlo[kFbGroup], s_hhi[kFbGroup];
   __shared__ uint64_t s_thh[kFbGroup], s_thl[kFbGroup];
+  __shared__ unsigned int s_nst, s_qcnt[kFbGroup], s_qbase[kFbGroup];
   unsigned int* s_hist = reinterpret_cast<unsigned int*>(sm);                        // HIST
   unsigned int (*s_cnt)[kFbBins + 1] = reinterpret_cast<unsigned int (*)[kFbBins + 1]>(sm);
   unsigned long long (*s_min)[kFbBins + 1] =
@@ -1102,6 +1109,8 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       const int q = threadIdx.x;
       // the prefilter bound: pairs below it cannot reach the threshold key's score
       s_tc[q] = (q < nqg && active[qg0 + q]) ? unord64(th_hi[qg0 + q]) - eps[qg0 + q] : INFINITY;
+      s_qcnt[q] = 0u;
+      if (q == 0) s_nst = 0u;
       if (q < nqg) {              // (the admission test's per-query values, read per pair)
         s_qn[q] = qnorm[qg0 + q];
         s_thh[q] = th_hi[qg0 + q];
@@ -1128,6 +1137,10 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   // most kPairBatch - 1 left over + 4 x 64 per tile); entry = row << 8 | group-local query
   uint64_t* pq = reinterpret_cast<uint64_t*>(sm + FB) + wave * kPairQueue;
   int qn = 0;
+  uint64_t* st_h = reinterpret_cast<uint64_t*>(sm + FBQ0);            // key hi
+  uint32_t* st_row = reinterpret_cast<uint32_t*>(st_h + kStage);      // row (key lo = ~row)
+  uint16_t* st_q = reinterpret_cast<uint16_t*>(st_row + kStage);      // group-local query
+  uint16_t* st_rank = st_q + kStage;                                  // slot within its query
   // the exact fp64 cosine of np (<= kPairBatch) queued pairs at once: every lane's 8-wide
   // pieces of all the pairs' rows are loaded together (one memory round trip instead of one per
   // pair), each pair in K6's summation order (so bit-identical to K4 / K6); lane p then runs
@@ -1169,10 +1182,17 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       const uint64_t h = ord64(sc);
       const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)my_row);
       if (h > s_thh[my_q] || (h == s_thh[my_q] && l >= s_thl[my_q])) {
-        const unsigned int pos = atomicAdd(&cnt[q], 1u);
-        if (pos < (unsigned int)cap) {
-          buf_hi[(size_t)q * cap + pos] = h;
-          buf_lo[(size_t)q * cap + pos] = l;
+        const unsigned int e = atomicAdd(&s_nst, 1u);
+        if (e < (unsigned int)kStage) {
+          st_h[e] = h;
+          st_row[e] = (uint32_t)my_row;
+          st_q[e] = (uint16_t)my_q;
+        } else {                                     // (stage full: straight to the buffer)
+          const unsigned int pos = atomicAdd(&cnt[q], 1u);
+          if (pos < (unsigned int)cap) {
+            buf_hi[(size_t)q * cap + pos] = h;
+            buf_lo[(size_t)q * cap + pos] = l;
+          }
         }
         const double lo = s_hlo[my_q], hi = s_hhi[my_q];
         int b = kFbBins;
@@ -1279,6 +1299,22 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       if (c) atomicAdd(&c_hist[(size_t)qg0 * kFbHistBins + i], c);
     }
   } else {
+    // the staged keys: ranks within their query (LDS), one slot reservation per query, stores
+    const int nst = (int)min(s_nst, (unsigned int)kStage);
+    for (int e = threadIdx.x; e < nst; e += blockDim.x) st_rank[e] = (uint16_t)atomicAdd(&s_qcnt[st_q[e]], 1u);
+    __syncthreads();
+    if (threadIdx.x < nqg && s_qcnt[threadIdx.x])
+      s_qbase[threadIdx.x] = atomicAdd(&cnt[qg0 + threadIdx.x], s_qcnt[threadIdx.x]);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nst; e += blockDim.x) {
+      const int ql_ = st_q[e];
+      const unsigned int pos = s_qbase[ql_] + st_rank[e];
+      if (pos < (unsigned int)cap) {
+        const size_t o = (size_t)(qg0 + ql_) * cap + pos;
+        buf_hi[o] = st_h[e];
+        buf_lo[o] = (uint64_t)(0xFFFFFFFFu - st_row[e]);
+      }
+    }
     for (int i = threadIdx.x; i < nqg * (kFbBins + 1); i += blockDim.x) {
       const unsigned int c = (&s_cnt[0][0])[i];
       if (c) {
