@@ -244,6 +244,9 @@ int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStre
   if (!attr) return hcr_set_error(HCR_EHIP, "bitonic_lds_kernel: LDS attribute");
   const int M = P < kSortChunk ? P : kSortChunk;
   const size_t lds = (size_t)2 * M * 8;
+  // (r06: a register form -- eight keys per thread, strides 1-256 in registers and wave shuffles,
+  // only the 10 strides >= 512 through LDS -- measured 159 µs against this kernel's 129 at the
+  // bench's 64 x 8192 sort, and was removed)
   hipLaunchKernelGGL(bitonic_lds_kernel, dim3((unsigned)(P / M), (unsigned)nseg), dim3(kBitonicThreads), lds, st, hi, lo, P, M,
                      M, 1);
   HIPC(hipGetLastError());

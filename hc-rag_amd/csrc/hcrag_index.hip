@@ -78,7 +78,7 @@ struct hcr_index {
       w_unc, w_cnt, w_tauest, w_umax, w_sk, w_pcnt, w_mcnt;
   // exact fallback workspace (K6/K7)
   DevBuf f_idx, f_q, f_qn, f_thh, f_thl, f_act, f_cnt, f_bufh, f_bufl, f_again, f_hlo, f_hhi,
-      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est, f_sorth, f_sortl;
+      f_hcnt, f_hmin, f_qhat, f_eps, f_ch, f_tmp, f_est, f_sorth, f_sortl, f_pairs, f_pcnt;
   hcr_search_stats stats{};
   int opt_qw1 = -1;             // HCR_OPT_QW1
   int opt_stride = 0;           // HCR_OPT_SAMPLE_STRIDE (0: the heuristic)
@@ -87,6 +87,14 @@ struct hcr_index {
   int opt_qw_dm = -1;           // HCR_OPT_QW_DM (-1: the default)
   int opt_qw_min = 0;           // HCR_OPT_QW_MIN (0: the heuristic)
   int opt_qw_stagger = -1;      // HCR_OPT_QW_STAGGER (-1: the default)
+  int opt_flag_read = 0;        // HCR_OPT_FLAG_READ (0: the default)
+  // the pass's certificate flags as the device leaves them in host memory (pinned, coherent,
+  // mapped): [0] sequence number, [1] uncertified queries, [2] out-of-index keys
+  int* h_flag = nullptr;
+  int* h_flag_dev = nullptr;
+  int flag_seq = 0;
+  int* pass_hflag = nullptr;          // set for the pass's finish / rescore launch: its last block
+  int pass_seq = 0;                   // stores the flags (HCR_OPT_FLAG_READ 3 / 4)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // ingest from a caller's stream (hcr_index_add_device): recorded there, waited on before
@@ -159,8 +167,10 @@ extern "C" int hcr_index_destroy(hcr_index* ix) {
                    &ix->w_pcnt, &ix->w_mcnt,
                    &ix->f_idx, &ix->f_q, &ix->f_qn, &ix->f_thh, &ix->f_thl, &ix->f_act,
                    &ix->f_cnt, &ix->f_bufh, &ix->f_bufl, &ix->f_again, &ix->f_hlo, &ix->f_hhi,
-                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est, &ix->f_sorth, &ix->f_sortl};
+                   &ix->f_hcnt, &ix->f_hmin, &ix->f_qhat, &ix->f_eps, &ix->f_ch, &ix->f_tmp, &ix->f_est, &ix->f_sorth, &ix->f_sortl,
+                   &ix->f_pairs, &ix->f_pcnt};
   for (DevBuf* b : all) b->release();
+  if (ix->h_flag) (void)hipHostFree(ix->h_flag);
   if (ix->ev_ingest) (void)hipEventDestroy(ix->ev_ingest);
   if (ix->ev0) (void)hipEventDestroy(ix->ev0);
   if (ix->ev1) (void)hipEventDestroy(ix->ev1);
@@ -483,6 +493,10 @@ extern "C" int hcr_index_set_option(hcr_index* ix, int option, int value) {
         return set_err(HCR_EINVAL, "HCR_OPT_QS_FORM value %d not 0, 1 or 3", value);
       ix->opt_qs = value;
       return HCR_OK;
+    case HCR_OPT_FLAG_READ:
+      if (value < 0 || value > 4) return set_err(HCR_EINVAL, "HCR_OPT_FLAG_READ value %d not in [0, 4]", value);
+      ix->opt_flag_read = value;
+      return HCR_OK;
     default:
       return set_err(HCR_EINVAL, "unknown index option %d", option);
   }
@@ -574,6 +588,10 @@ struct TestHooks {
   bool no_prepass = false, rigorous_seed = false, prepass_topk = false, debug_cfg = false;
   bool no_finish = false;            // HCRAG_NO_FINISH: separate merge + rescore launches
   bool no_mfma_filter = false;       // HCRAG_NO_MFMA_FILTER: the fallback's scans on K6 (fp64 only)
+  bool k6_inline = false;            // HCRAG_K6_INLINE: K6m rescoring inline (no K6c / K6r)
+  int64_t k6_pcap = 0;               // HCRAG_K6_PCAP: pair slots per group (tests: force overflow)
+  int k6_chunks = 0;                 // HCRAG_K6_CHUNKS: K6 scan blocks per query group (A/B)
+  int k6r_blocks = 0;                // HCRAG_K6R_BLOCKS: K6r blocks per query group (A/B)
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -587,6 +605,10 @@ static const TestHooks& hooks() {
     t.debug_cfg = getenv("HCRAG_DEBUG_CFG") != nullptr;
     t.no_finish = getenv("HCRAG_NO_FINISH") != nullptr;
     t.no_mfma_filter = getenv("HCRAG_NO_MFMA_FILTER") != nullptr;
+    t.k6_inline = getenv("HCRAG_K6_INLINE") != nullptr;
+    if (const char* e = getenv("HCRAG_K6_PCAP")) t.k6_pcap = std::max<int64_t>(1, atoll(e));
+    if (const char* e = getenv("HCRAG_K6_CHUNKS")) t.k6_chunks = std::max(8, atoi(e));
+    if (const char* e = getenv("HCRAG_K6R_BLOCKS")) t.k6r_blocks = std::max(1, atoi(e));
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -795,7 +817,8 @@ static void launch_rescore(hcr_index* ix, const uint64_t* merged, const float* d
                      ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
-                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound);
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound, ix->pass_hflag,
+                     ix->pass_seq);
 }
 
 // Merge of the last <= G lists + rescore in one launch (finish_kernel); false when its LDS
@@ -817,7 +840,8 @@ static int launch_finish(hcr_index* ix, const uint64_t* lists, const int* cnt, i
                      ix->rows.as<const TS>(), ix->ld, ix->n, ix->norm64.as<const double>(), k, mode, thr,
                      ix->id_offset, out_s, out_i, ix->w_unc.as<int>(), ix->w_cnt.as<int>(),
                      ix->w_tauest.as<const uint32_t>(), ix->w_sk.as<uint64_t>(),
-                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound);
+                     ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr, ix->gs_bound, ix->pass_hflag,
+                     ix->pass_seq);
   HIPC(hipGetLastError());
   return HCR_OK;
 }
@@ -1039,6 +1063,71 @@ static double accum_gamma(int ld) {
   const double u = std::ldexp(1.0, -24);
   const double nu = (ld + 1) * u;
   return nu / (1.0 - nu) + 4.0 * u;
+}
+
+// The pass's one host read (the certificate count and the bounds-check flag, w_cnt[0..1]); the
+// stream's work is complete when it returns.  HCR_OPT_FLAG_READ: 1 = hipMemcpyAsync into pageable
+// memory + hipStreamSynchronize (r05), 2 = the same into pinned memory, 3 / 4 = the last block of
+// the pass's finish / rescore launch stores the flags and a sequence number into pinned coherent
+// host memory (flags_prepare sets it up before that launch) and the host spins on the sequence
+// number (no copy engine, no runtime wait, no extra launch), checking the stream for an error
+// every 4096 polls; 3 then synchronises the stream (idle by then), 4 (the default) does not: the
+// store comes after every other write of the pass.
+static int flag_mode(const hcr_index* ix) { return ix->opt_flag_read == 0 ? 4 : ix->opt_flag_read; }
+static int flags_prepare(hcr_index* ix) {
+  ix->pass_hflag = nullptr;
+  if (flag_mode(ix) == 1) return HCR_OK;
+  if (!ix->h_flag) {
+    void* h = nullptr;
+    HIPC(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(h, 0, 64);
+    void* dp = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dp, h, 0);
+    if (e != hipSuccess) {
+      (void)hipHostFree(h);
+      return set_err(HCR_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    ix->h_flag = static_cast<int*>(h);
+    ix->h_flag_dev = static_cast<int*>(dp);
+  }
+  if (flag_mode(ix) >= 3) {
+    ix->pass_seq = ix->flag_seq = (ix->flag_seq % 0x3FFFFFFF) + 1;
+    ix->pass_hflag = ix->h_flag_dev;
+  }
+  return HCR_OK;
+}
+static int read_pass_flags(hcr_index* ix, hipStream_t st, int* out) {
+  const int mode = flag_mode(ix);
+  ix->pass_hflag = nullptr;
+  if (mode == 1) {
+    HIPC(hipMemcpyAsync(out, ix->w_cnt.p, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    return HCR_OK;
+  }
+  if (mode == 2) {
+    HIPC(hipMemcpyAsync(ix->h_flag + 1, ix->w_cnt.p, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    out[0] = ix->h_flag[1];
+    out[1] = ix->h_flag[2];
+    return HCR_OK;
+  }
+  const int seq = ix->pass_seq;
+  for (unsigned it = 1;; ++it) {
+    if (__atomic_load_n(ix->h_flag, __ATOMIC_ACQUIRE) == seq) break;
+    if ((it & 4095u) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {                // (done: the stores are visible by now)
+        if (__atomic_load_n(ix->h_flag, __ATOMIC_ACQUIRE) == seq) break;
+        return set_err(HCR_EINTERNAL, "internal: the pass's finish launch completed without its flag store");
+      }
+      if (q != hipErrorNotReady) return set_err(HCR_EHIP, "search stream: %s", hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
+  out[0] = __atomic_load_n(ix->h_flag + 1, __ATOMIC_RELAXED);
+  out[1] = __atomic_load_n(ix->h_flag + 2, __ATOMIC_RELAXED);
+  if (mode == 3) HIPC(hipStreamSynchronize(st));
+  return HCR_OK;
 }
 
 // One pipeline pass over nq (<= kQueryChunk) device queries at candidate depth kp.
@@ -1281,6 +1370,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
                        const_cast<int*>(lcnt), (uint32_t)ix->n + 7u);
     HIPC(hipGetLastError());
   }
+  CHECK(flags_prepare(ix));            // (the finish / rescore launch's last block stores the flags)
   // fused for small batches (configs[1], B = 256: 0.372 vs 0.376 ms per search); above
   // 512 queries the separate launches (W = 8 rank shape, B = 1024: 1.973-1.985 vs
   // 1.985-1.998 ms: the fused block's merge LDS cuts the rescore's residency; r03f A/B)
@@ -1306,8 +1396,7 @@ static int search_pass(hcr_index* ix, const float* d_q, int nq, int k, int mode,
   }
 
   int cnt2[2] = {0, 0};     // [0] uncertified queries, [1] candidate keys outside the index
-  HIPC(hipMemcpyAsync(cnt2, ix->w_cnt.p, 8, hipMemcpyDeviceToHost, st));
-  HIPC(hipStreamSynchronize(st));
+  CHECK(read_pass_flags(ix, st, cnt2));
   if (cnt2[1] != 0)
     return set_err(HCR_EINTERNAL, "internal: a candidate key names a row outside the index (%lld rows); "
                    "the search was abandoned", (long long)ix->n);
@@ -1401,6 +1490,50 @@ hist_seed_kernel(const unsigned int* __restrict__ hist, const double* __restrict
   }
 }
 
+// A fallback group's per-query state in one launch, a block per query (r06: six host-to-device
+// copies, a memset and the query gather before, ~45 µs of the deep path's time line): from `up`
+// ([ng] starting thresholds, then [ng] chunk-local query indices) or, up = nullptr, thresholds 0
+// for queries idx0 + i; thl 0, active, no estimate, the first round's histogram range [the
+// threshold's score (below -1 without one), just above 1], the query's fp32 row gathered into
+// fq, and (ch != nullptr) its K6h histogram zeroed.
+__global__ void __launch_bounds__(256)
+fb_group_init_kernel(int ng, const uint64_t* __restrict__ up, int idx0, const float* __restrict__ qc, int dim,
+                     int* __restrict__ idx, uint64_t* __restrict__ thh, uint64_t* __restrict__ thl,
+                     int* __restrict__ act, int* __restrict__ est, double* __restrict__ hlo,
+                     double* __restrict__ hhi, float* __restrict__ fq, unsigned int* __restrict__ ch) {
+  const int i = blockIdx.x;
+  if (i >= ng) return;
+  const uint64_t t = up ? up[i] : 0ull;
+  const int qi = up ? (int)up[ng + i] : idx0 + i;
+  if (threadIdx.x == 0) {
+    idx[i] = qi;
+    thh[i] = t;
+    thl[i] = 0ull;
+    act[i] = 1;
+    est[i] = 0;
+    hlo[i] = t == 0ull ? -1.0 - 1e-6 : unord64(t);
+    hhi[i] = 1.0 + 1e-6;
+  }
+  for (int j = threadIdx.x; j < dim; j += blockDim.x) fq[(int64_t)i * dim + j] = qc[(int64_t)qi * dim + j];
+  if (ch)
+    for (int j = threadIdx.x; j < kFbHistBins; j += blockDim.x) ch[(size_t)i * kFbHistBins + j] = 0u;
+}
+
+// A fallback round's counters in one launch (four memsets before, ~5 µs of time line each):
+// admissions, the re-run count, the histograms, K6c's pair counts.
+__global__ void fb_round_init_kernel(int ng, unsigned int* __restrict__ cnt, int* __restrict__ again,
+                                     unsigned int* __restrict__ hcnt, unsigned long long* __restrict__ hmin, int nh,
+                                     unsigned long long* __restrict__ pcnt, int npc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nh) {
+    hcnt[i] = 0u;
+    hmin[i] = ~0ull;
+  }
+  if (i < ng) cnt[i] = 0u;
+  if (i == 0) *again = 0;
+  if (pcnt && i < npc) pcnt[i] = 0ull;
+}
+
 static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>& idx,
                           const std::vector<uint64_t>& sk, int k, int mode, double thr, double* os,
                           int64_t* oi, hipStream_t st, int64_t cap64 = kFallbackCap) {
@@ -1422,14 +1555,21 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   // MFMA-prefiltered scans take up to kFbGroupsPerScan query groups at once (one pass over the
   // rows for all of them); the fp64 scan (K6) one group
   int super = mf ? kFallbackGroup * kFbGroupsPerScan : kFallbackGroup;
-  if (big) {             // (the deep path's buffers per query: cap admitted + P sorted pairs)
-    const int64_t per_q = (cap64 + P) * 16;
+  // K6c's compacted pair list per query group (kFbGroup x cap slots: a group that admits more
+  // coarse pairs is rescanned by the inline K6m)
+  const bool two_launch = mf && !hooks().k6_inline;
+  const int64_t pcap = hooks().k6_pcap > 0 ? hooks().k6_pcap : (int64_t)kFallbackGroup * cap64;
+  if (big) {             // (the deep path's buffers per query: cap admitted + P sorted pairs + pairs)
+    const int64_t per_q = (cap64 + P) * 16 + (two_launch ? cap64 * 8 : 0);
     const int64_t fit = std::max<int64_t>(1, (int64_t)(kDeepBudget / (size_t)per_q));
     super = (int)std::min<int64_t>(super, fit >= kFallbackGroup ? fit / kFallbackGroup * kFallbackGroup : fit);
   }
-  const int64_t mchunks = round_up(std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32, 2048)), 8);
-#define MFIL(TS, KS, HIST)                                                                        \
-  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, HIST>), dim3((unsigned)(mchunks * ngr)), dim3(256), 0, st, \
+  // (MFMA scans: 512 row chunks per query group -- 2 x 512 blocks at the bench's 64 queries, two
+  // rounds of blocks at their LDS: r06ac, deep k = 5000 1.32 -> 1.24 ms against 2048 chunks)
+  const int64_t mchunks = round_up(std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32,
+                                                                          hooks().k6_chunks ? hooks().k6_chunks : 512)), 8);
+#define MFIL(TS, KS, MODE)                                                                        \
+  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, MODE>), dim3(grid), dim3(256), 0, st,           \
                      ix->f_qhat.as<const TS>(), ix->f_eps.as<const double>(), ix->f_q.as<const float>(), \
                      ng, ix->dim, ix->f_qn.as<const double>(), ix->rows.as<const TS>(), ix->ld, ix->n, \
                      ix->inv32.as<const float>(), ix->norm64.as<const double>(),                 \
@@ -1439,15 +1579,25 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>(),        \
-                     ix->f_ch.as<unsigned int>(), ngr, hstride)
-#define MFIL_KS(TS, HIST)                                                                         \
+                     ix->f_ch.as<unsigned int>(), ngr, hstride, pairs, pcnt, pcap)
+#define MFIL_KS(TS, MODE)                                                                         \
   do {                                                                                            \
-    if (ksteps == 12) MFIL(TS, 12, HIST); else if (ksteps == 24) MFIL(TS, 24, HIST); else MFIL(TS, 32, HIST); \
+    if (ksteps == 12) MFIL(TS, 12, MODE); else if (ksteps == 24) MFIL(TS, 24, MODE); else MFIL(TS, 32, MODE); \
   } while (0)
-  auto launch_mfil = [&](int ng, bool hist, int hstride) {
+#define MFIL_MODE(TS)                                                                             \
+  do {                                                                                            \
+    if (kmode == kK6Hist) MFIL_KS(TS, kK6Hist); else if (kmode == kK6Compact) MFIL_KS(TS, kK6Compact); \
+    else if (kmode == kK6Rescore) MFIL_KS(TS, kK6Rescore); else MFIL_KS(TS, kK6Inline);               \
+  } while (0)
+  // kmode: kK6Hist / kK6Inline (pairs = nullptr: every group) / the two-launch form (K6c, K6r,
+  // then the inline K6m for the groups whose pair list overflowed)
+  auto launch_mfil = [&](int ng, int kmode, int hstride, uint64_t* pairs, unsigned long long* pcnt) {
     const int ngr = (ng + kFallbackGroup - 1) / kFallbackGroup;
-    if (ix->dtype == HCR_F16) { if (hist) MFIL_KS(_Float16, true); else MFIL_KS(_Float16, false); }
-    else { if (hist) MFIL_KS(__bf16, true); else MFIL_KS(__bf16, false); }
+    // (K6r: ~2048 blocks over the groups -- 8 waves per CU at its LDS, a few rounds)
+    const int rb = hooks().k6r_blocks ? hooks().k6r_blocks : 512;
+    const unsigned grid = (unsigned)(kmode == kK6Rescore ? ngr * rb : mchunks * ngr);
+    if (ix->dtype == HCR_F16) MFIL_MODE(_Float16);
+    else MFIL_MODE(__bf16);
   };
   for (size_t g0 = 0; g0 < idx.size(); g0 += super) {
     const int ng = (int)std::min<size_t>(super, idx.size() - g0);
@@ -1467,34 +1617,47 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
       CHECK(ix->f_sortl.ensure((size_t)ng * P * 8));
     }
     CHECK(ix->f_again.ensure(16));
+    if (two_launch) {
+      CHECK(ix->f_pcnt.ensure((size_t)kFbGroupsPerScan * 8 + 64));
+      CHECK(ix->f_pairs.ensure((size_t)((ng + kFallbackGroup - 1) / kFallbackGroup) * (size_t)pcap * 8));
+    }
     CHECK(ix->f_hlo.ensure((size_t)ng * 8));
     CHECK(ix->f_hhi.ensure((size_t)ng * 8));
     CHECK(ix->f_hcnt.ensure((size_t)ng * (kFbBins + 1) * 4));
     CHECK(ix->f_hmin.ensure((size_t)ng * (kFbBins + 1) * 8));
-    std::vector<uint64_t> thh(sk.begin() + g0, sk.begin() + g0 + ng), thl(ng, 0ull);
-    std::vector<int> act(ng, 1), est(ng, 0);
-    // histogram range of the first round: [score of the starting threshold, just above 1]
-    std::vector<double> hlo(ng), hhi(ng, 1.0 + 1e-6);
-    for (int i = 0; i < ng; ++i) {
-      if (thh[i] == 0ull) { hlo[i] = -1.0 - 1e-6; continue; }
-      const uint64_t u = thh[i];
-      const uint64_t b = (u & 0x8000000000000000ull) ? (u ^ 0x8000000000000000ull) : ~u;
-      double v;
-      memcpy(&v, &b, 8);
-      hlo[i] = v;
+    const std::vector<uint64_t> thh(sk.begin() + g0, sk.begin() + g0 + ng);
+    // the group's state on the device: queries g0 .. g0 + ng - 1 without starting thresholds (the
+    // deep path, k > 256) need no upload; otherwise one copy of [thresholds | query indices]
+    bool plain = true;
+    for (int i = 0; i < ng && plain; ++i) plain = thh[i] == 0ull && idx[g0 + i] == (int)g0 + i;
+    const uint64_t* up = nullptr;
+    std::vector<uint64_t> upl;
+    if (!plain) {
+      CHECK(ix->f_tmp.ensure((size_t)round_up(ng, kFallbackGroup) * 24 + 64));   // (the prep's size below)
+      upl.resize((size_t)ng * 2);
+      for (int i = 0; i < ng; ++i) {
+        upl[i] = thh[i];
+        upl[ng + i] = (uint64_t)idx[g0 + i];
+      }
+      HIPC(hipMemcpyAsync(ix->f_tmp.p, upl.data(), (size_t)ng * 16, hipMemcpyHostToDevice, st));
+      up = ix->f_tmp.as<const uint64_t>();
     }
-    HIPC(hipMemcpyAsync(ix->f_hlo.p, hlo.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(ix->f_hhi.p, hhi.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(ix->f_idx.p, idx.data() + g0, (size_t)ng * 4, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(ix->f_thh.p, thh.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(ix->f_thl.p, thl.data(), (size_t)ng * 8, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(ix->f_act.p, act.data(), (size_t)ng * 4, hipMemcpyHostToDevice, st));
-    HIPC(hipMemsetAsync(ix->f_est.p, 0, (size_t)ng * 4, st));
-    hipLaunchKernelGGL(gather_rows_f32, dim3(ng), dim3(256), 0, st, qc, ix->f_idx.as<const int>(), ng,
-                       ix->dim, ix->f_q.as<float>());
-    hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
-                       ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
+    // round 0 (K6h) for the queries without a starting threshold (MFMA prefilter only)
+    bool need0 = false;
+    for (int i = 0; i < ng; ++i) need0 |= thh[i] == 0ull;
+    need0 = need0 && mf;
+    if (need0) CHECK(ix->f_ch.ensure((size_t)ngpad * kFbHistBins * 4));
+    hipLaunchKernelGGL(fb_group_init_kernel, dim3((unsigned)ng), dim3(256), 0, st, ng, up, (int)g0, qc, ix->dim,
+                       ix->f_idx.as<int>(), ix->f_thh.as<uint64_t>(), ix->f_thl.as<uint64_t>(), ix->f_act.as<int>(),
+                       ix->f_est.as<int>(), ix->f_hlo.as<double>(), ix->f_hhi.as<double>(), ix->f_q.as<float>(),
+                       need0 ? ix->f_ch.as<unsigned int>() : nullptr);
     HIPC(hipGetLastError());
+    // (the MFMA route's prep writes the fp64 query norms, the same sum as query_norms_kernel's)
+    if (!mf) {
+      hipLaunchKernelGGL(query_norms_kernel, dim3((ng + 3) / 4), dim3(256), 0, st,
+                         ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<double>());
+      HIPC(hipGetLastError());
+    }
     if (mf) {
       // the groups' unit MFMA-dtype queries and eps_q for the non-UNIT coarse score c =
       // fl(q^.e . inv32); padded to whole groups with zero queries
@@ -1505,19 +1668,16 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
 #define PREP(TM)                                                                                   \
   hipLaunchKernelGGL((prep_queries_kernel<TM>), dim3((ngpad + 3) / 4), dim3(256), 0, st,           \
                      ix->f_q.as<const float>(), ng, ngpad, ix->dim, ix->ld, ix->f_qhat.as<TM>(),    \
-                     reinterpret_cast<double*>(tmp), ix->f_eps.as<double>(), ix->rho_host,            \
+                     ix->f_qn.as<double>(), ix->f_eps.as<double>(), ix->rho_host,                     \
                      accum_gamma(ix->ld), -1.0, reinterpret_cast<uint32_t*>(tmp + (size_t)ngpad * 8), \
                      reinterpret_cast<uint32_t*>(tmp + (size_t)ngpad * 12),                          \
                      reinterpret_cast<int*>(tmp + (size_t)ngpad * 16))
       if (ix->dtype == HCR_F16) PREP(_Float16); else PREP(__bf16);
 #undef PREP
       HIPC(hipGetLastError());
-      bool need0 = false;
-      for (int i = 0; i < ng; ++i) need0 |= thh[i] == 0ull;
       if (need0) {
         // round 0 (K6h): coarse histograms -> a starting threshold T_q <= the true k-th best
-        CHECK(ix->f_ch.ensure((size_t)ngpad * kFbHistBins * 4));
-        HIPC(hipMemsetAsync(ix->f_ch.p, 0, (size_t)ng * kFbHistBins * 4, st));
+        // (zeroed by fb_group_init_kernel)
         // on a corpus of >= 100 k rows per sampled stride (10M rows, k <= 6250: 16), a sample
         // of runs of 4 16-row tiles, one in hstride: an estimated threshold (see K6h)
         int hstride = 1;
@@ -1528,7 +1688,7 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
         const double fk = frac * k;
         const uint64_t need_rows = hstride == 1 ? (uint64_t)k
                                                 : (uint64_t)std::ceil(fk + 5.0 * std::sqrt(fk) + 3.0);
-        launch_mfil(ng, true, hstride);
+        launch_mfil(ng, kK6Hist, hstride, nullptr, nullptr);
         HIPC(hipGetLastError());
         hipLaunchKernelGGL(hist_seed_kernel, dim3((unsigned)ng), dim3(64), 0, st, ix->f_ch.as<const unsigned int>(),
                            ix->f_eps.as<const double>(), ng, (unsigned long long)need_rows, hstride > 1 ? 1 : 0,
@@ -1543,10 +1703,13 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
     while (again > 0) {
       if (++rounds > kFallbackMaxRounds)
         return set_err(HCR_EHIP, "internal: exact fallback did not converge in %d rounds", kFallbackMaxRounds);
-      HIPC(hipMemsetAsync(ix->f_cnt.p, 0, (size_t)ng * 4, st));
-      HIPC(hipMemsetAsync(ix->f_again.p, 0, 4, st));
-      HIPC(hipMemsetAsync(ix->f_hcnt.p, 0, (size_t)ng * (kFbBins + 1) * 4, st));
-      HIPC(hipMemsetAsync(ix->f_hmin.p, 0xFF, (size_t)ng * (kFbBins + 1) * 8, st));
+      const int ngr = (ng + kFallbackGroup - 1) / kFallbackGroup;
+      const int nh = ng * (kFbBins + 1);
+      hipLaunchKernelGGL(fb_round_init_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, ng,
+                         ix->f_cnt.as<unsigned int>(), ix->f_again.as<int>(), ix->f_hcnt.as<unsigned int>(),
+                         ix->f_hmin.as<unsigned long long>(), nh,
+                         two_launch ? ix->f_pcnt.as<unsigned long long>() : nullptr, ngr);
+      HIPC(hipGetLastError());
 #define FIL(TS)                                                                                  \
   hipLaunchKernelGGL((exact_filter_kernel<TS>), dim3(fgrid), dim3(256), 0, st,                  \
                      ix->f_q.as<const float>(), ng, ix->dim, ix->f_qn.as<const double>(),       \
@@ -1557,7 +1720,15 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_bufh.as<uint64_t>(), ix->f_bufl.as<uint64_t>(),                       \
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>())
-      if (mf) launch_mfil(ng, false, 1);
+      if (two_launch) {
+        uint64_t* pr = ix->f_pairs.as<uint64_t>();
+        unsigned long long* pc = ix->f_pcnt.as<unsigned long long>();
+        launch_mfil(ng, kK6Compact, 1, pr, pc);
+        launch_mfil(ng, kK6Rescore, 1, pr, pc);
+        launch_mfil(ng, kK6Inline, 1, pr, pc);
+      } else if (mf) {
+        launch_mfil(ng, kK6Inline, 1, nullptr, nullptr);
+      }
       else if (ix->dtype == HCR_F16) FIL(_Float16); else if (ix->dtype == HCR_BF16) FIL(__bf16); else FIL(float);
 #undef FIL
       if (big)
@@ -1591,6 +1762,7 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
       HIPC(hipStreamSynchronize(st));
     }
   }
+#undef MFIL_MODE
 #undef MFIL_KS
 #undef MFIL
   return HCR_OK;

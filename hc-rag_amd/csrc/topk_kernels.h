@@ -748,7 +748,7 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
                                               int64_t* __restrict__ out_i, int* __restrict__ unc_flags,
                                               int* __restrict__ unc_count, const uint32_t* __restrict__ tau_est,
                                               uint64_t* __restrict__ sk_out, const int64_t* __restrict__ idmap,
-                                              double* __restrict__ bound_out) {
+                                              double* __restrict__ bound_out, int* hflag, int hseq) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // Every row this block dereferences (norm64, rows, idmap) comes from a candidate key.  A key
   // whose row lies outside the index can only come from a defect upstream (a score-kernel or
@@ -859,6 +859,23 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
     out_i[(size_t)q * k + t] = id;
   }
   HCR_FIN_STAMP(5);
+  // the pass's flags to the host (HCR_OPT_FLAG_READ 3 / 4, r06): the last block to finish -- a
+  // ticket in unc_count[2], reset by prep_queries_kernel -- stores unc_count[0..1] into the
+  // pinned host words, then the sequence number the host polls (system scope, vector stores)
+  if (hflag) {
+    __syncthreads();                                 // (this block's flag atomics are done)
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(unc_count + 2, 1) == (int)gridDim.x - 1) {
+        __threadfence();
+        const int c0 = __hip_atomic_load(unc_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int c1 = __hip_atomic_load(unc_count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(hflag + 1, c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hflag + 2, c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hflag, hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 #define HCR_RESCORE_PARAMS                                                                          \
@@ -867,10 +884,11 @@ __device__ __forceinline__ void rescore_block(uint64_t* keys, const double* qd, 
       const double *__restrict__ norm64, int k, int mode, double thr, int64_t id_offset,            \
       double *__restrict__ out_s, int64_t *__restrict__ out_i, int *__restrict__ unc_flags,         \
       int *__restrict__ unc_count, const uint32_t *__restrict__ tau_est,                            \
-      uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap, double *__restrict__ bound_out
+      uint64_t *__restrict__ sk_out, const int64_t *__restrict__ idmap, double *__restrict__ bound_out, \
+      int *hflag, int hseq
 #define HCR_RESCORE_ARGS                                                                            \
   q, kp, dim, qnorm, eps, rows, ld, n_rows, norm64, k, mode, thr, id_offset, out_s, out_i, unc_flags,      \
-      unc_count, tau_est, sk_out, idmap, bound_out
+      unc_count, tau_est, sk_out, idmap, bound_out, hflag, hseq
 
 // K4 on a merged list ([q][kp] keys in global memory, merge_lists' last level).
 // LDS: dim x 8 (query) + kp x 32 + 16.
@@ -1055,6 +1073,14 @@ constexpr int kPairQueue = kPairBatch - 1 + 4 * 64 + 1;
 // was one of two dependent round trips in every rescore batch); one atomic per query and block
 // at the end reserves their slots; past kStage the pairs append to global memory directly
 constexpr int kStage = 384;
+// K6 modes (r06): the inline scan (K6m: every admitted pair rescored by the scanning wave), the
+// coarse histogram (K6h), and the two-launch form of K6m -- K6c compacts the coarse-admitted
+// (row, query) pairs of every query group into a global list per group, K6r rescores that list
+// with every wave of the chip (no scan beside it: the rescoring's row gathers no longer stall the
+// stream), the group's admissions, staging and histograms exactly as K6m's.  A group whose list
+// overflowed its pcap slots is skipped by K6r and scanned by the inline K6m instead (launched
+// after it, only that group's blocks do any work).
+enum { kK6Inline = 0, kK6Hist = 1, kK6Compact = 2, kK6Rescore = 3 };
 
 __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1062,7 +1088,7 @@ __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename TS, int KS, bool HIST>
+template <typename TS, int KS, int MODE>
 __global__ void __launch_bounds__(256)
 exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__ eps,
                          const float* __restrict__ q32, int nq, int dim,
@@ -1074,16 +1100,18 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
                          uint64_t* __restrict__ buf_hi, uint64_t* __restrict__ buf_lo,
                          const double* __restrict__ h_lo, const double* __restrict__ h_hi,
                          unsigned int* __restrict__ h_cnt, unsigned long long* __restrict__ h_min,
-                         unsigned int* __restrict__ c_hist, int ngroups, int hstride) {
+                         unsigned int* __restrict__ c_hist, int ngroups, int hstride,
+                         uint64_t* __restrict__ pairs, unsigned long long* __restrict__ pcnt, int64_t pcap) {
+  constexpr bool HIST = MODE == kK6Hist, COMPACT = MODE == kK6Compact, RESC = MODE == kK6Rescore;
   using Op = MfmaOp<TS>;
   using V = typename Op::V;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
   constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
-  constexpr size_t FBQ0 = FB + (size_t)4 * kPairQueue * 8;           // + the pair queues
+  constexpr size_t FBQ0 = FB + (RESC ? 0 : (size_t)4 * kPairQueue * 8);   // + the pair queues
   constexpr size_t FBQ = FBQ0 + (size_t)kStage * (8 + 4 + 2 + 2);     // + the staged keys
   static_assert(FB % 8 == 0, "pair queue alignment");
   static_assert(FBQ <= 65536, "K6m LDS");
-  __shared__ __attribute__((aligned(16))) char sm[HB > FBQ ? HB : FBQ];
+  __shared__ __attribute__((aligned(16))) char sm[RESC ? FBQ : (HB > FBQ ? HB : FBQ)];
   __shared__ double s_tc[kFbGroup], s_qn[kFbGroup], s_hlo[kFbGroup], s_hhi[kFbGroup];
   __shared__ uint64_t s_thh[kFbGroup], s_thl[kFbGroup];
   __shared__ unsigned int s_nst, s_qcnt[kFbGroup], s_qbase[kFbGroup];
@@ -1094,14 +1122,19 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   // block -> (query group, row chunk): the ngroups groups of one row chunk are consecutive
   // blocks of one XCD (round-robin dispatch), so each row tile comes from HBM once per scan and
   // from that XCD's L2 for the other groups (the grid is a multiple of 8 x ngroups)
+  // (K6r: block b rescores pairs of group b % ngroups; no row chunks)
   const int xcd = blockIdx.x & 7, rr = blockIdx.x >> 3;
-  const int grp = rr % ngroups, chunk = (rr / ngroups) * 8 + xcd;
+  const int grp = RESC ? (int)(blockIdx.x % ngroups) : rr % ngroups;
+  const int chunk = RESC ? (int)(blockIdx.x / ngroups) : (rr / ngroups) * 8 + xcd;
   const int nchunks = gridDim.x / ngroups;
   const int qg0 = grp * kFbGroup, nqg = min(kFbGroup, nq - qg0);
+  // the two-launch form: K6r takes a group whose list fits, the inline K6m one that overflowed
+  if (RESC && (pcnt[grp] == 0ull || pcnt[grp] > (unsigned long long)pcap)) return;
+  if (MODE == kK6Inline && pcnt && pcnt[grp] <= (unsigned long long)pcap) return;
   if constexpr (HIST) {
     for (int i = threadIdx.x; i < kFbGroup * kFbHistBins; i += blockDim.x) s_hist[i] = 0u;
   } else {
-    for (int i = threadIdx.x; i < kFbGroup * (kFbBins + 1); i += blockDim.x) {
+    for (int i = threadIdx.x; !COMPACT && i < kFbGroup * (kFbBins + 1); i += blockDim.x) {
       (&s_cnt[0][0])[i] = 0u;
       (&s_min[0][0])[i] = ~0ull;
     }
@@ -1126,7 +1159,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   const int ql = qb * 16 + (lane & 15);              // the lane's query (accumulator column)
   // query fragments: lane l holds q^[qb*16 + (l & 15)][32 ks + 8 (l >> 4) .. + 8)
   V qf[KS];
-  {
+  if constexpr (!RESC) {
     const TS* src = qhat + (size_t)(qg0 + ql) * ld + (lane >> 4) * 8;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
@@ -1137,6 +1170,23 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   // most kPairBatch - 1 left over + 4 x 64 per tile); entry = row << 8 | group-local query
   uint64_t* pq = reinterpret_cast<uint64_t*>(sm + FB) + wave * kPairQueue;
   int qn = 0;
+  // K6c: a queue per wave over the whole LDS array (no histograms, no staging in this mode),
+  // flushed to the group's global list -- one returning atomic per flush -- when a tile could
+  // overflow it
+  constexpr int PQC = (int)((HB > FBQ ? HB : FBQ) / 8 / 4);
+  static_assert(PQC >= 2 * 4 * 64, "K6c queue");
+  uint64_t* pqc = reinterpret_cast<uint64_t*>(sm) + wave * PQC;
+  uint64_t* pg = pairs ? pairs + (size_t)grp * (size_t)pcap : nullptr;
+  auto flush_pairs = [&]() __attribute__((always_inline)) {
+    lds_wave_sync();
+    unsigned long long base = 0ull;
+    if (lane == 0) base = atomicAdd(&pcnt[grp], (unsigned long long)qn);
+    base = __shfl(base, 0);
+    for (int i = lane; i < qn; i += 64)
+      if (base + (unsigned long long)i < (unsigned long long)pcap) pg[base + i] = pqc[i];
+    qn = 0;
+    lds_wave_sync();
+  };
   uint64_t* st_h = reinterpret_cast<uint64_t*>(sm + FBQ0);            // key hi
   uint32_t* st_row = reinterpret_cast<uint32_t*>(st_h + kStage);      // row (key lo = ~row)
   uint16_t* st_q = reinterpret_cast<uint16_t*>(st_row + kStage);      // group-local query
@@ -1145,11 +1195,12 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   // pieces of all the pairs' rows are loaded together (one memory round trip instead of one per
   // pair), each pair in K6's summation order (so bit-identical to K4 / K6); lane p then runs
   // pair p's key test, append and histogram
+  constexpr int PB = RESC ? 8 : kPairBatch;      // (K6r: 8 pairs per wave at a time)
   auto rescore_batch = [&](const uint64_t* e, int np) __attribute__((always_inline)) {
-    int64_t prow[kPairBatch];
-    int pqs[kPairBatch];
+    int64_t prow[PB];
+    int pqs[PB];
 #pragma unroll
-    for (int p = 0; p < kPairBatch; ++p) {
+    for (int p = 0; p < PB; ++p) {
       const uint64_t v = e[p < np ? p : 0];
       prow[p] = (int64_t)(v >> 8);
       pqs[p] = (int)(v & 255u);
@@ -1157,22 +1208,22 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     int64_t my_row = prow[0];
     int my_q = pqs[0];
 #pragma unroll
-    for (int p = 1; p < kPairBatch; ++p)
+    for (int p = 1; p < PB; ++p)
       if (lane == p) { my_row = prow[p]; my_q = pqs[p]; }
     const double nr = lane < np ? norm64[my_row] : 1.0;
-    double ex[kPairBatch];
+    double ex[PB];
 #pragma unroll
-    for (int p = 0; p < kPairBatch; ++p) ex[p] = 0.0;
+    for (int p = 0; p < PB; ++p) ex[p] = 0.0;
     for (int d0 = lane * 8; d0 < dim; d0 += 512) {
-      float x[kPairBatch][8];
+      float x[PB][8];
 #pragma unroll
-      for (int p = 0; p < kPairBatch; ++p) load8_f32(rows + prow[p] * ld + d0, x[p]);
+      for (int p = 0; p < PB; ++p) load8_f32(rows + prow[p] * ld + d0, x[p]);
 #pragma unroll
-      for (int p = 0; p < kPairBatch; ++p) acc8_f64(ex[p], q32 + (int64_t)(qg0 + pqs[p]) * dim, d0, dim, x[p]);
+      for (int p = 0; p < PB; ++p) acc8_f64(ex[p], q32 + (int64_t)(qg0 + pqs[p]) * dim, d0, dim, x[p]);
     }
     double my_ex = 0.0;
 #pragma unroll
-    for (int p = 0; p < kPairBatch; ++p) {
+    for (int p = 0; p < PB; ++p) {
       const double t = wave_sum_f64(ex[p]);
       if (lane == p) my_ex = t;
     }
@@ -1205,7 +1256,13 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       }
     }
   };
-  const int64_t ntile = (n + 15) / 16;
+  if constexpr (RESC) {
+    // K6r: the group's compacted pairs, PB per wave at a time, grid-strided
+    const int64_t npt = (int64_t)pcnt[grp];
+    for (int64_t p0 = ((int64_t)chunk * 4 + wave) * PB; p0 < npt; p0 += (int64_t)nchunks * 4 * PB)
+      rescore_batch(pg + p0, (int)min((int64_t)PB, npt - p0));
+  }
+  const int64_t ntile = RESC ? 0 : (n + 15) / 16;
   const int64_t stride = (int64_t)nchunks * 2;
   // (HIST: runs of 4 tiles out of every 4 hstride -- a sample of the rows when hstride > 1)
   auto tile_of = [&](int64_t tv) -> int64_t {
@@ -1226,7 +1283,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       if (b * CH + j < KS) a[j] = *reinterpret_cast<const V*>(ra + (b * CH + j) * 32);
   };
   int64_t tv = (int64_t)chunk * 2 + (wave >> 1);
-  if (tile_of(tv) < ntile) load_batch(frag_ptr(tile_of(tv)), 0);
+  if (!RESC && tile_of(tv) < ntile) load_batch(frag_ptr(tile_of(tv)), 0);
   for (;; tv += stride) {
     const int64_t t = tile_of(tv);
     if (t >= ntile) break;
@@ -1262,6 +1319,21 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
         b = b < 0 ? 0 : b >= kFbHistBins ? kFbHistBins - 1 : b;
         atomicAdd(&s_hist[ql * kFbHistBins + b], 1u);
       }
+    } else if constexpr (COMPACT) {
+      // admitted pairs go to the wave's queue, flushed to the group's list
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool adm = rok[r] && (double)(acc[r] * iv[r]) >= tcq;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(adm);
+        if (adm) {
+          const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          pqc[qn + below] = ((uint64_t)(rb + r) << 8) | (uint64_t)ql;
+        }
+        qn += __builtin_popcountll(m);
+      }
+      qn = __builtin_amdgcn_readfirstlane(qn);
+      if (qn > PQC - 4 * 64) flush_pairs();
     } else {
       // admitted pairs go to the wave's queue; full batches of kPairBatch are rescored at once
 #pragma unroll
@@ -1286,7 +1358,11 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       }
     }
   }
-  if constexpr (!HIST) {
+  if constexpr (COMPACT) {
+    if (qn > 0) flush_pairs();
+    return;
+  }
+  if constexpr (MODE == kK6Inline) {
     if (qn > 0) {
       lds_wave_sync();
       rescore_batch(pq, qn);

@@ -214,6 +214,7 @@ class VectorIndex:
     OPT_QW_DM = 6
     OPT_QW_MIN = 7
     OPT_QW_STAGGER = 8
+    OPT_FLAG_READ = 9
 
     def set_option(self, option: int, value: int) -> None:
         """Kernel-choice option (``hcr_index_set_option``); never changes results.
@@ -224,7 +225,10 @@ class VectorIndex:
         ``VectorIndex.OPT_PREPASS``: sampling pre-pass kernel, 1 v4, 2 QW (0 heuristic).
         ``VectorIndex.OPT_QW_DM``: QW's stage LDS-DMA issue, -1 default, 0 at the barrier, 3 spread.
         ``VectorIndex.OPT_QW_MIN``: smallest batch on the QW kernel (0 heuristic).
-        ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 2, the default; 1 / 2 = two / one accumulator sets; 0 = off)."""
+        ``VectorIndex.OPT_QW_STAGGER``: QW at D = 384, waves 4-7's test one stage late (-1 = 2, the default; 1 / 2 = two / one accumulator sets; 0 = off).
+        ``VectorIndex.OPT_FLAG_READ``: the pass's certificate-count read back: 1 pageable copy, 2 pinned
+        copy, 3 / 4 a kernel store into pinned host memory polled by the host (with / without a stream
+        synchronisation after it); 0 the default."""
         check(lib().hcr_index_set_option(self._h, int(option), int(value)))
 
     TEST_PLANT_BAD_KEY = 1

@@ -208,10 +208,15 @@ int hcr_index_set_timing(hcr_index* index, int enable);
  *   HCR_OPT_QW_MIN: the smallest batch the QW kernel takes (0 = the heuristic: 129).
  *   HCR_OPT_QW_STAGGER: QW at D = 384 -- waves 4-7 run each stage's top-k' test one stage
  *                late (beside the other waves' MFMAs): 1 = with two accumulator sets, 2 = with
- *                one, 0 = off, -1 = the default (2). */
+ *                one, 0 = off, -1 = the default (2).
+ *   HCR_OPT_FLAG_READ: how a search pass reads its certificate count back (its one host read):
+ *                1 = a copy into pageable memory + stream synchronisation, 2 = a copy into
+ *                pinned memory + synchronisation, 3 = a one-thread kernel stores it into pinned
+ *                coherent host memory with a sequence number the host polls, then synchronises,
+ *                4 = the same without the synchronisation; 0 = the default. */
 typedef enum { HCR_OPT_QW1 = 1, HCR_OPT_SAMPLE_STRIDE = 3, HCR_OPT_QS_FORM = 4,
                HCR_OPT_PREPASS = 5, HCR_OPT_QW_DM = 6, HCR_OPT_QW_MIN = 7,
-               HCR_OPT_QW_STAGGER = 8 } hcr_index_option;
+               HCR_OPT_QW_STAGGER = 8, HCR_OPT_FLAG_READ = 9 } hcr_index_option;
                /* (2: removed in 0.3) */
 int hcr_index_set_option(hcr_index* index, int option, int value);
 

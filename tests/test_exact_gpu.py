@@ -425,6 +425,52 @@ def test_out_of_range_candidate_key_is_an_error(hc, B):
         _check(s, i, es, ei)
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 0])
+def test_flag_read_modes(hc, mode):
+    """HCR_OPT_FLAG_READ (r06: how a pass reads its certificate count and bounds-check flag back):
+    every mode returns the oracle's lists, reports a planted out-of-index key as HCR_EINTERNAL,
+    and sees the uncertified count of a duplicate cluster (the widened pass / fallback runs)."""
+    from hcrag_amd._lib import HCR_EINTERNAL, HcrError
+    rng = np.random.default_rng(77 + mode)
+    N, D, k, B = 30000, 384, 10, 64
+    E = rng.standard_normal((N, D)).astype(np.float32)
+    E[100:400] = E[7]                       # 301 exact duplicates: q = E[7] cannot certify at k'
+    Q = rng.standard_normal((B, D)).astype(np.float32)
+    Q[0] = E[7]
+    with hc.VectorIndex(D, "f16") as ix:
+        ix.set_option(ix.OPT_FLAG_READ, mode)
+        ix.add(E, normalize=True)
+        R = ix.get_rows()
+        es, ei = O.cosine_topk(Q, R, k)
+        for _ in range(3):
+            s, i = ix.search(Q, k)
+            _check(s, i, es, ei)
+        st = ix.last_stats()
+        assert st["widened_queries"] + st["fallback_queries"] >= 1, st
+        ix.test_hook(ix.TEST_PLANT_BAD_KEY, 1)
+        try:
+            with pytest.raises(HcrError) as exc:
+                ix.search(Q, k)
+        finally:
+            ix.test_hook(ix.TEST_PLANT_BAD_KEY, 0)
+        assert exc.value.code == HCR_EINTERNAL, exc.value
+        s, i = ix.search(Q, k)
+        _check(s, i, es, ei)
+
+
+@pytest.mark.parametrize("env", [{"HCRAG_K6_INLINE": "1"}, {}, {"HCRAG_K6_PCAP": "100"}])
+def test_k6_admission_forms(env):
+    """r06: the exact fallback's admission scan inline (K6m), as two launches (K6c compaction +
+    K6r rescoring, the default), and with every group's pair list overflowing (the inline K6m
+    rescans those groups after K6r) -- identical to the oracle (tests/k6_forms_check.py)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "k6_forms_check.py")],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "parity ok" in r.stdout
+
+
 def test_deep_k_sorted_scan(hc):
     """VERDICT r4 missing #4: k > 2048 (the reference's argsort(...)[::-1][:top_k] takes any
     top_k, experiments/main.py:844,889) on the deep path (r06: the exact fallback's admission

@@ -36,9 +36,9 @@ I = torch.empty((B, K), dtype=torch.int64, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 names = {"QW1": ix.OPT_QW1, "SAMPLE_STRIDE": ix.OPT_SAMPLE_STRIDE, "QS_FORM": ix.OPT_QS_FORM,
          "PREPASS": ix.OPT_PREPASS, "QW_DM": ix.OPT_QW_DM, "QW_MIN": ix.OPT_QW_MIN,
-         "QW_STAGGER": ix.OPT_QW_STAGGER}
+         "QW_STAGGER": ix.OPT_QW_STAGGER, "FLAG_READ": ix.OPT_FLAG_READ}
 defaults = {"QW1": -1, "SAMPLE_STRIDE": 0, "QS_FORM": 0, "PREPASS": 0, "QW_DM": -1, "QW_MIN": 0,
-            "QW_STAGGER": -1}
+            "QW_STAGGER": -1, "FLAG_READ": 0}
 
 
 def apply(arm):
