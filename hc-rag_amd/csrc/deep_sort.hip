@@ -93,7 +93,11 @@ __device__ void kth_pair_desc(const uint64_t* __restrict__ h, const uint64_t* __
 
 // K7b: one block per query of the group (see the file comment).  sort_hi / sort_lo: [nq][P]
 // (P = a power of two >= k) receive a finished query's k best keys, unsorted, 0-padded.
-__global__ void __launch_bounds__(256)
+// r06: a query whose admitted keys fit kSelLds pairs is selected from an LDS copy of its buffer
+// (one global read instead of one per radix pass and one for the compaction; 1024 threads).
+constexpr int kSelLds = 8192;
+constexpr int kSelThreads = 1024;
+__global__ void __launch_bounds__(kSelThreads)
 select_big_kernel(int k, int cap, int P, const unsigned int* __restrict__ cnt,
                   const uint64_t* __restrict__ buf_hi, const uint64_t* __restrict__ buf_lo,
                   uint64_t* __restrict__ th_hi, uint64_t* __restrict__ th_lo, int* __restrict__ active,
@@ -158,6 +162,15 @@ select_big_kernel(int k, int cap, int P, const unsigned int* __restrict__ cnt,
     return;
   }
   // every admitted row is in the buffer: its top min(k, c) keys are the answer
+  if (c <= (unsigned int)kSelLds) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t sm_sb[];
+    uint64_t* lh = sm_sb;
+    uint64_t* ll = sm_sb + kSelLds;
+    for (int i = threadIdx.x; i < (int)c; i += blockDim.x) { lh[i] = bh[i]; ll[i] = bl[i]; }
+    __syncthreads();
+    bh = lh;
+    bl = ll;
+  }
   const int kk = (int)min(c, (unsigned int)k);
   uint64_t kh = 0ull, kl = 0ull;
   if ((int)c > kk) kth_pair_desc(bh, bl, (int)c, kk, 32, s_hist, s_res, s_misc, &kh, &kl);
@@ -267,7 +280,12 @@ int hcr_launch_select_big(int nq, int k, int cap, int P, const unsigned int* cnt
                           const uint64_t* buf_lo, uint64_t* th_hi, uint64_t* th_lo, int* active, int* n_again,
                           double* h_lo, double* h_hi, const unsigned int* h_cnt, const unsigned long long* h_min,
                           int* est, uint64_t* sort_hi, uint64_t* sort_lo, hipStream_t st) {
-  hipLaunchKernelGGL(select_big_kernel, dim3((unsigned)nq), dim3(256), 0, st, k, cap, P, cnt, buf_hi, buf_lo, th_hi,
+  static const bool attr = hipFuncSetAttribute((const void*)select_big_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               2 * kSelLds * 8) == hipSuccess;
+  if (!attr) return hcr_set_error(HCR_EHIP, "select_big_kernel: LDS attribute");
+  hipLaunchKernelGGL(select_big_kernel, dim3((unsigned)nq), dim3(kSelThreads), (size_t)2 * kSelLds * 8, st, k, cap, P,
+                     cnt, buf_hi, buf_lo, th_hi,
                      th_lo, active, n_again, h_lo, h_hi, h_cnt, h_min, est, sort_hi, sort_lo);
   HIPC(hipGetLastError());
   return HCR_OK;

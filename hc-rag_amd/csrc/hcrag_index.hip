@@ -592,6 +592,7 @@ struct TestHooks {
   int64_t k6_pcap = 0;               // HCRAG_K6_PCAP: pair slots per group (tests: force overflow)
   int k6_chunks = 0;                 // HCRAG_K6_CHUNKS: K6 scan blocks per query group (A/B)
   int k6r_blocks = 0;                // HCRAG_K6R_BLOCKS: K6r blocks per query group (A/B)
+  bool k6_qb1 = false;               // HCRAG_K6_QB1: K6h / K6c with one query half per wave (A/B)
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -609,6 +610,7 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_K6_PCAP")) t.k6_pcap = std::max<int64_t>(1, atoll(e));
     if (const char* e = getenv("HCRAG_K6_CHUNKS")) t.k6_chunks = std::max(8, atoi(e));
     if (const char* e = getenv("HCRAG_K6R_BLOCKS")) t.k6r_blocks = std::max(1, atoi(e));
+    t.k6_qb1 = getenv("HCRAG_K6_QB1") != nullptr;
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -1568,8 +1570,8 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
   // rounds of blocks at their LDS: r06ac, deep k = 5000 1.32 -> 1.24 ms against 2048 chunks)
   const int64_t mchunks = round_up(std::max<int64_t>(1, std::min<int64_t>((ix->n + 31) / 32,
                                                                           hooks().k6_chunks ? hooks().k6_chunks : 512)), 8);
-#define MFIL(TS, KS, MODE)                                                                        \
-  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, MODE>), dim3(grid), dim3(256), 0, st,           \
+#define MFIL(TS, KS, MODE, QB)                                                                    \
+  hipLaunchKernelGGL((exact_filter_mfma_kernel<TS, KS, MODE, QB>), dim3(grid), dim3(256), 0, st,       \
                      ix->f_qhat.as<const TS>(), ix->f_eps.as<const double>(), ix->f_q.as<const float>(), \
                      ng, ix->dim, ix->f_qn.as<const double>(), ix->rows.as<const TS>(), ix->ld, ix->n, \
                      ix->inv32.as<const float>(), ix->norm64.as<const double>(),                 \
@@ -1580,14 +1582,18 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                      ix->f_hlo.as<const double>(), ix->f_hhi.as<const double>(),                \
                      ix->f_hcnt.as<unsigned int>(), ix->f_hmin.as<unsigned long long>(),        \
                      ix->f_ch.as<unsigned int>(), ngr, hstride, pairs, pcnt, pcap)
-#define MFIL_KS(TS, MODE)                                                                         \
+#define MFIL_KS(TS, MODE, QB)                                                                     \
   do {                                                                                            \
-    if (ksteps == 12) MFIL(TS, 12, MODE); else if (ksteps == 24) MFIL(TS, 24, MODE); else MFIL(TS, 32, MODE); \
+    if (ksteps == 12) MFIL(TS, 12, MODE, QB); else if (ksteps == 24) MFIL(TS, 24, MODE, QB);     \
+    else MFIL(TS, 32, MODE, QB);                                                                  \
   } while (0)
+  // (the scan-only modes with both query halves per wave, QB = 2; HCRAG_K6_QB1: one, A/B)
 #define MFIL_MODE(TS)                                                                             \
   do {                                                                                            \
-    if (kmode == kK6Hist) MFIL_KS(TS, kK6Hist); else if (kmode == kK6Compact) MFIL_KS(TS, kK6Compact); \
-    else if (kmode == kK6Rescore) MFIL_KS(TS, kK6Rescore); else MFIL_KS(TS, kK6Inline);               \
+    const bool qb1 = hooks().k6_qb1;                                                              \
+    if (kmode == kK6Hist) { if (qb1) MFIL_KS(TS, kK6Hist, 1); else MFIL_KS(TS, kK6Hist, 2); }    \
+    else if (kmode == kK6Compact) { if (qb1) MFIL_KS(TS, kK6Compact, 1); else MFIL_KS(TS, kK6Compact, 2); } \
+    else if (kmode == kK6Rescore) MFIL_KS(TS, kK6Rescore, 1); else MFIL_KS(TS, kK6Inline, 1);    \
   } while (0)
   // kmode: kK6Hist / kK6Inline (pairs = nullptr: every group) / the two-launch form (K6c, K6r,
   // then the inline K6m for the groups whose pair list overflowed)
@@ -1748,19 +1754,24 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
                            ix->f_hhi.as<double>(), ix->f_hcnt.as<const unsigned int>(),
                            ix->f_hmin.as<const unsigned long long>(), ix->f_est.as<int>());
       HIPC(hipGetLastError());
+      if (big) {
+        // the sort of the k answers and the outputs, enqueued before the round's re-run count is
+        // read (r06: the read-back, sync and launch had the sort wait ~40 µs for the host): a query
+        // that finished in this or an earlier round holds its k keys in its sort segment (K7b
+        // writes a segment only in the round its query finishes); a query still active gets its
+        // segment sorted and emitted again after the round that finishes it, which is the last
+        // write of its outputs.  Usually the first K6m round finishes every query.
+        CHECK(hcr_seg_sort_desc_pairs(ix->f_sorth.as<uint64_t>(), ix->f_sortl.as<uint64_t>(), ng, P, st));
+        CHECK(hcr_launch_deep_emit(ng, ix->f_sorth.as<const uint64_t>(), ix->f_sortl.as<const uint64_t>(), P, k,
+                                   mode, thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
+                                   ix->f_idx.as<const int>(), os, oi, st));
+      }
+      // (K7 / the deep emit write the outputs before this sync: they are final when the search
+      // call returns, hcrag.h)
       HIPC(hipMemcpyAsync(&again, ix->f_again.p, 4, hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));
     }
     ix->stats.fallback_rounds += rounds;
-    if (big) {             // every query of the group holds its k answers: sort them, emit
-      CHECK(hcr_seg_sort_desc_pairs(ix->f_sorth.as<uint64_t>(), ix->f_sortl.as<uint64_t>(), ng, P, st));
-      CHECK(hcr_launch_deep_emit(ng, ix->f_sorth.as<const uint64_t>(), ix->f_sortl.as<const uint64_t>(), P, k, mode,
-                                 thr, ix->id_offset, ix->has_idmap ? ix->idmap.as<const int64_t>() : nullptr,
-                                 ix->f_idx.as<const int>(), os, oi, st));
-      // (K7 writes its outputs inside the round loop, before its stream sync; these come after
-      // it: the outputs are final when the search call returns, hcrag.h)
-      HIPC(hipStreamSynchronize(st));
-    }
   }
 #undef MFIL_MODE
 #undef MFIL_KS

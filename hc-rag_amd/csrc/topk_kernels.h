@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <typename TS, int KS, int MODE>
+template <typename TS, int KS, int MODE, int QB = 1>
 __global__ void __launch_bounds__(256)
 exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__ eps,
                          const float* __restrict__ q32, int nq, int dim,
@@ -1103,12 +1103,18 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
                          unsigned int* __restrict__ c_hist, int ngroups, int hstride,
                          uint64_t* __restrict__ pairs, unsigned long long* __restrict__ pcnt, int64_t pcap) {
   constexpr bool HIST = MODE == kK6Hist, COMPACT = MODE == kK6Compact, RESC = MODE == kK6Rescore;
+  // QB = 2 (the scan-only modes K6h / K6c, r06): every wave holds both 16-query halves of the
+  // group and multiplies each tile's A fragments with both -- a tile is loaded by one wave instead
+  // of two, and the block's 4 waves take 4 different tiles
+  static_assert(QB == 1 || HIST || COMPACT, "QB = 2: the scan-only modes");
   using Op = MfmaOp<TS>;
   using V = typename Op::V;
   constexpr size_t HB = (size_t)kFbGroup * kFbHistBins * 4;
   constexpr size_t FB = (size_t)kFbGroup * (kFbBins + 1) * 12;
   constexpr size_t FBQ0 = FB + (RESC ? 0 : (size_t)4 * kPairQueue * 8);   // + the pair queues
-  constexpr size_t FBQ = FBQ0 + (size_t)kStage * (8 + 4 + 2 + 2);     // + the staged keys
+  // (K6r: a block rescores ~500 pairs at the bench's deep k -- a larger stage, still 2 blocks per CU)
+  constexpr int STG = RESC ? 960 : kStage;
+  constexpr size_t FBQ = FBQ0 + (size_t)STG * (8 + 4 + 2 + 2);     // + the staged keys
   static_assert(FB % 8 == 0, "pair queue alignment");
   static_assert(FBQ <= 65536, "K6m LDS");
   __shared__ __attribute__((aligned(16))) char sm[RESC ? FBQ : (HB > FBQ ? HB : FBQ)];
@@ -1157,15 +1163,23 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qb = wave & 1;
   const int ql = qb * 16 + (lane & 15);              // the lane's query (accumulator column)
-  // query fragments: lane l holds q^[qb*16 + (l & 15)][32 ks + 8 (l >> 4) .. + 8)
-  V qf[KS];
-  if constexpr (!RESC) {
-    const TS* src = qhat + (size_t)(qg0 + ql) * ld + (lane >> 4) * 8;
+  // query fragments: lane l holds q^[qb*16 + (l & 15)][32 ks + 8 (l >> 4) .. + 8) (QB = 2: both
+  // halves, qlb[b] = b*16 + (l & 15))
+  V qf[QB][KS];
+  int qlb[QB];
+  bool qokb[QB];
+  double tcqb[QB];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const V*>(src + ks * 32);
+  for (int b = 0; b < QB; ++b) {
+    qlb[b] = QB == 1 ? ql : b * 16 + (lane & 15);
+    if constexpr (!RESC) {
+      const TS* src = qhat + (size_t)(qg0 + qlb[b]) * ld + (lane >> 4) * 8;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) qf[b][ks] = *reinterpret_cast<const V*>(src + ks * 32);
+    }
+    qokb[b] = qlb[b] < nqg && active[qg0 + qlb[b]];
+    tcqb[b] = HIST ? 0.0 : s_tc[qlb[b]];
   }
-  const bool qok = ql < nqg && active[qg0 + ql];
-  const double tcq = HIST ? 0.0 : s_tc[ql];
   // K6m's admitted (row, query) pairs: a queue per wave in the LDS above the histograms (at
   // most kPairBatch - 1 left over + 4 x 64 per tile); entry = row << 8 | group-local query
   uint64_t* pq = reinterpret_cast<uint64_t*>(sm + FB) + wave * kPairQueue;
@@ -1188,9 +1202,9 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     lds_wave_sync();
   };
   uint64_t* st_h = reinterpret_cast<uint64_t*>(sm + FBQ0);            // key hi
-  uint32_t* st_row = reinterpret_cast<uint32_t*>(st_h + kStage);      // row (key lo = ~row)
-  uint16_t* st_q = reinterpret_cast<uint16_t*>(st_row + kStage);      // group-local query
-  uint16_t* st_rank = st_q + kStage;                                  // slot within its query
+  uint32_t* st_row = reinterpret_cast<uint32_t*>(st_h + STG);      // row (key lo = ~row)
+  uint16_t* st_q = reinterpret_cast<uint16_t*>(st_row + STG);      // group-local query
+  uint16_t* st_rank = st_q + STG;                                  // slot within its query
   // the exact fp64 cosine of np (<= kPairBatch) queued pairs at once: every lane's 8-wide
   // pieces of all the pairs' rows are loaded together (one memory round trip instead of one per
   // pair), each pair in K6's summation order (so bit-identical to K4 / K6); lane p then runs
@@ -1214,19 +1228,38 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     double ex[PB];
 #pragma unroll
     for (int p = 0; p < PB; ++p) ex[p] = 0.0;
+    // (r06: the query's 8 floats as two 16-byte loads when the rows of q32 are 16-byte aligned;
+    // the same values, so acc8_f64's order and bits)
+    const bool qvec = (dim & 7) == 0;
     for (int d0 = lane * 8; d0 < dim; d0 += 512) {
       float x[PB][8];
 #pragma unroll
       for (int p = 0; p < PB; ++p) load8_f32(rows + prow[p] * ld + d0, x[p]);
 #pragma unroll
-      for (int p = 0; p < PB; ++p) acc8_f64(ex[p], q32 + (int64_t)(qg0 + pqs[p]) * dim, d0, dim, x[p]);
+      for (int p = 0; p < PB; ++p) {
+        const float* qp = q32 + (int64_t)(qg0 + pqs[p]) * dim;
+        if (qvec) {
+          float qv[8];
+          const float4 u = reinterpret_cast<const float4*>(qp + d0)[0], w = reinterpret_cast<const float4*>(qp + d0)[1];
+          qv[0] = u.x; qv[1] = u.y; qv[2] = u.z; qv[3] = u.w; qv[4] = w.x; qv[5] = w.y; qv[6] = w.z; qv[7] = w.w;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ex[p] += (double)qv[j] * (double)x[p][j];
+        } else {
+          acc8_f64(ex[p], qp, d0, dim, x[p]);
+        }
+      }
     }
+    // the PB wave sums side by side, level by level (wave_sum_f64's pairing and order: the same
+    // bits; one after another each shuffle waited for the last)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+      for (int p = 0; p < PB; ++p)
+        ex[p] += __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(ex[p]), m));
     double my_ex = 0.0;
 #pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const double t = wave_sum_f64(ex[p]);
-      if (lane == p) my_ex = t;
-    }
+    for (int p = 0; p < PB; ++p)
+      if (lane == p) my_ex = ex[p];
     if (lane < np) {
       const int q = qg0 + my_q;
       const double sc = my_ex / (s_qn[my_q] * nr);
@@ -1234,7 +1267,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       const uint64_t l = (uint64_t)(0xFFFFFFFFu - (uint32_t)my_row);
       if (h > s_thh[my_q] || (h == s_thh[my_q] && l >= s_thl[my_q])) {
         const unsigned int e = atomicAdd(&s_nst, 1u);
-        if (e < (unsigned int)kStage) {
+        if (e < (unsigned int)STG) {
           st_h[e] = h;
           st_row[e] = (uint32_t)my_row;
           st_q[e] = (uint16_t)my_q;
@@ -1263,7 +1296,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
       rescore_batch(pg + p0, (int)min((int64_t)PB, npt - p0));
   }
   const int64_t ntile = RESC ? 0 : (n + 15) / 16;
-  const int64_t stride = (int64_t)nchunks * 2;
+  const int64_t stride = (int64_t)nchunks * (QB == 2 ? 4 : 2);
   // (HIST: runs of 4 tiles out of every 4 hstride -- a sample of the rows when hstride > 1)
   auto tile_of = [&](int64_t tv) -> int64_t {
     return HIST ? (tv >> 2) * (4 * (int64_t)hstride) + (tv & 3) : tv;
@@ -1282,58 +1315,71 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     for (int j = 0; j < CH; ++j)
       if (b * CH + j < KS) a[j] = *reinterpret_cast<const V*>(ra + (b * CH + j) * 32);
   };
-  int64_t tv = (int64_t)chunk * 2 + (wave >> 1);
+  int64_t tv = QB == 2 ? (int64_t)chunk * 4 + wave : (int64_t)chunk * 2 + (wave >> 1);
   if (!RESC && tile_of(tv) < ntile) load_batch(frag_ptr(tile_of(tv)), 0);
   for (;; tv += stride) {
     const int64_t t = tile_of(tv);
     if (t >= ntile) break;
     const int64_t r0 = t * 16;
     const int64_t tn = tile_of(tv + stride);
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    floatx4 accb[QB];
+#pragma unroll
+    for (int qbi = 0; qbi < QB; ++qbi) accb[qbi] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int64_t rb = r0 + (lane >> 4) * 4;         // the lane's 4 rows: rb .. rb + 3
     float iv[4];
-    bool rok[4];
+    bool rowok[4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
 #pragma unroll
       for (int j = 0; j < CH; ++j)
-        if (b * CH + j < KS) acc = Op::run(a[j], qf[b * CH + j], acc);
+#pragma unroll
+        for (int qbi = 0; qbi < QB; ++qbi)
+          if (b * CH + j < KS) accb[qbi] = Op::run(a[j], qf[qbi][b * CH + j], accb[qbi]);
       if (b + 1 < NB) {
         load_batch(frag_ptr(t), b + 1);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = rb + r;
-          rok[r] = qok && row < n && (!maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u));
+          rowok[r] = row < n && (!maskbits || ((maskbits[row >> 5] >> (row & 31)) & 1u));
           iv[r] = row < n ? inv32[row] : 0.f;
         }
         if (tn < ntile) load_batch(frag_ptr(tn), 0);
       }
     }
+    const floatx4 acc = accb[0];
+    bool rok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rok[r] = rowok[r] && qokb[0];
+    const double tcq = tcqb[0];
     if constexpr (HIST) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!rok[r]) continue;
-        const float c = acc[r] * iv[r];
-        int b = (int)floorf((c + kFbHistRange) * ((float)kFbHistBins / (2.f * kFbHistRange)));
-        b = b < 0 ? 0 : b >= kFbHistBins ? kFbHistBins - 1 : b;
-        atomicAdd(&s_hist[ql * kFbHistBins + b], 1u);
-      }
+      for (int qbi = 0; qbi < QB; ++qbi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!(rowok[r] && qokb[qbi])) continue;
+          const float c = accb[qbi][r] * iv[r];
+          int b = (int)floorf((c + kFbHistRange) * ((float)kFbHistBins / (2.f * kFbHistRange)));
+          b = b < 0 ? 0 : b >= kFbHistBins ? kFbHistBins - 1 : b;
+          atomicAdd(&s_hist[qlb[qbi] * kFbHistBins + b], 1u);
+        }
     } else if constexpr (COMPACT) {
       // admitted pairs go to the wave's queue, flushed to the group's list
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool adm = rok[r] && (double)(acc[r] * iv[r]) >= tcq;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(adm);
-        if (adm) {
-          const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          pqc[qn + below] = ((uint64_t)(rb + r) << 8) | (uint64_t)ql;
+      for (int qbi = 0; qbi < QB; ++qbi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool adm = rowok[r] && qokb[qbi] && (double)(accb[qbi][r] * iv[r]) >= tcqb[qbi];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(adm);
+          if (adm) {
+            const int below = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            pqc[qn + below] = ((uint64_t)(rb + r) << 8) | (uint64_t)qlb[qbi];
+          }
+          qn += __builtin_popcountll(m);
         }
-        qn += __builtin_popcountll(m);
-      }
       qn = __builtin_amdgcn_readfirstlane(qn);
-      if (qn > PQC - 4 * 64) flush_pairs();
+      if (qn > PQC - 4 * 64 * QB) flush_pairs();
     } else {
       // admitted pairs go to the wave's queue; full batches of kPairBatch are rescored at once
 #pragma unroll
@@ -1376,7 +1422,7 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
     }
   } else {
     // the staged keys: ranks within their query (LDS), one slot reservation per query, stores
-    const int nst = (int)min(s_nst, (unsigned int)kStage);
+    const int nst = (int)min(s_nst, (unsigned int)STG);
     for (int e = threadIdx.x; e < nst; e += blockDim.x) st_rank[e] = (uint16_t)atomicAdd(&s_qcnt[st_q[e]], 1u);
     __syncthreads();
     if (threadIdx.x < nqg && s_qcnt[threadIdx.x])
