@@ -17,7 +17,9 @@
 //    (score desc, row / id asc) tie rule of the whole library holds.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #define HCR_TOPK_TEMPLATES_ONLY   // (topk_kernels.h: constants and device helpers only here)
 #include "hcrag.h"
@@ -255,7 +257,16 @@ int hcr_seg_sort_desc_pairs(uint64_t* hi, uint64_t* lo, int nseg, int P, hipStre
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                2 * kSortChunk * 8) == hipSuccess;
   if (!attr) return hcr_set_error(HCR_EHIP, "bitonic_lds_kernel: LDS attribute");
-  const int M = P < kSortChunk ? P : kSortChunk;
+  // chunk: the largest power of two <= kSortChunk that still gives >= 256 blocks (r06: the bench's
+  // deep k sorts 64 segments of 8192 -- one 8192-key block each left 192 CUs idle and the block
+  // LDS-bound); HCRAG_SORT_CHUNK overrides (A/B)
+  static const int chunk_env = getenv("HCRAG_SORT_CHUNK") ? atoi(getenv("HCRAG_SORT_CHUNK")) : 0;
+  int M = P < kSortChunk ? P : kSortChunk;
+  if (chunk_env >= 2 && (chunk_env & (chunk_env - 1)) == 0 && chunk_env <= kSortChunk) {
+    M = std::min(P, chunk_env);
+  } else {
+    while (M > 1024 && (int64_t)nseg * (P / M) < 256) M >>= 1;
+  }
   const size_t lds = (size_t)2 * M * 8;
   // (r06: a register form -- eight keys per thread, strides 1-256 in registers and wave shuffles,
   // only the 10 strides >= 512 through LDS -- measured 159 µs against this kernel's 129 at the

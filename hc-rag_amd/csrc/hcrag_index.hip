@@ -593,6 +593,7 @@ struct TestHooks {
   int k6_chunks = 0;                 // HCRAG_K6_CHUNKS: K6 scan blocks per query group (A/B)
   int k6r_blocks = 0;                // HCRAG_K6R_BLOCKS: K6r blocks per query group (A/B)
   bool k6_qb1 = false;               // HCRAG_K6_QB1: K6h / K6c with one query half per wave (A/B)
+  int k6h_ratio = 0;                 // HCRAG_K6H_RATIO: K6h sampling rule (A/B)
   int prepass_min_tiles = 0, sample_stride = 0, seed_rank = 0;
 };
 static const TestHooks& hooks() {
@@ -611,6 +612,7 @@ static const TestHooks& hooks() {
     if (const char* e = getenv("HCRAG_K6_CHUNKS")) t.k6_chunks = std::max(8, atoi(e));
     if (const char* e = getenv("HCRAG_K6R_BLOCKS")) t.k6r_blocks = std::max(1, atoi(e));
     t.k6_qb1 = getenv("HCRAG_K6_QB1") != nullptr;
+    if (const char* e = getenv("HCRAG_K6H_RATIO")) t.k6h_ratio = std::max(1, atoi(e));
     t.rigorous_seed = getenv("HCRAG_RIGOROUS_SEED") != nullptr;
     t.prepass_topk = getenv("HCRAG_PREPASS_TOPK") != nullptr;
     if (const char* e = getenv("HCRAG_PREPASS_MIN_TILES")) t.prepass_min_tiles = std::max(1, atoi(e));
@@ -1687,7 +1689,9 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
         // on a corpus of >= 100 k rows per sampled stride (10M rows, k <= 6250: 16), a sample
         // of runs of 4 16-row tiles, one in hstride: an estimated threshold (see K6h)
         int hstride = 1;
-        while (hstride < 16 && ix->n / (2 * hstride) >= (int64_t)100 * k) hstride *= 2;
+        // (HCRAG_K6H_RATIO: sampled rows per k the next stride must leave, default 100; A/B)
+        const int64_t ratio = hooks().k6h_ratio ? hooks().k6h_ratio : 100;
+        while (hstride < 16 && ix->n / (2 * hstride) >= ratio * k) hstride *= 2;
         const int64_t ntile16 = (ix->n + 15) / 16, run = 4 * (int64_t)hstride;
         const int64_t stiles = ntile16 / run * 4 + std::min<int64_t>(4, ntile16 % run);
         const double frac = std::min(1.0, (double)(stiles * 16) / (double)ix->n);

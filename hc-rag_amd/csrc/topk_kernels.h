@@ -1117,6 +1117,8 @@ exact_filter_mfma_kernel(const TS* __restrict__ qhat, const double* __restrict__
   constexpr size_t FBQ = FBQ0 + (size_t)STG * (8 + 4 + 2 + 2);     // + the staged keys
   static_assert(FB % 8 == 0, "pair queue alignment");
   static_assert(FBQ <= 65536, "K6m LDS");
+  // (K6c with only its pair queues in LDS, 32 KiB: 4 blocks per CU instead of 2, measured the same
+  // -- 224 vs 227 µs, r06ag -- and not kept: the scan is not bound by its occupancy)
   __shared__ __attribute__((aligned(16))) char sm[RESC ? FBQ : (HB > FBQ ? HB : FBQ)];
   __shared__ double s_tc[kFbGroup], s_qn[kFbGroup], s_hlo[kFbGroup], s_hhi[kFbGroup];
   __shared__ uint64_t s_thh[kFbGroup], s_thl[kFbGroup];
