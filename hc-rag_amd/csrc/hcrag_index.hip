@@ -7,6 +7,7 @@
 //   experiments/isRelevant.py:197-210  batch_semantic_similarity (all scores)        -> hcr_score_all
 //   llama-index SimpleVectorStore.query / get_top_k_embeddings (query_interface.py:200-204)
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cmath>
@@ -1126,7 +1127,10 @@ static int read_pass_flags(hcr_index* ix, hipStream_t st, int* out) {
       }
       if (q != hipErrorNotReady) return set_err(HCR_EHIP, "search stream: %s", hipGetErrorString(q));
     }
-    __builtin_ia32_pause();
+    // (past ~0.3 ms of polling -- the large batches' searches take milliseconds -- the thread
+    // yields its core between polls instead of spinning on it)
+    if (it > 16384u) sched_yield();
+    else __builtin_ia32_pause();
   }
   out[0] = __atomic_load_n(ix->h_flag + 1, __ATOMIC_RELAXED);
   out[1] = __atomic_load_n(ix->h_flag + 2, __ATOMIC_RELAXED);
