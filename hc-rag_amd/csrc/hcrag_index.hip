@@ -1690,11 +1690,13 @@ static int exact_fallback(hcr_index* ix, const float* qc, const std::vector<int>
       if (need0) {
         // round 0 (K6h): coarse histograms -> a starting threshold T_q <= the true k-th best
         // (zeroed by fb_group_init_kernel)
-        // on a corpus of >= 100 k rows per sampled stride (10M rows, k <= 6250: 16), a sample
+        // on a corpus of >= 12 k rows per sampled stride (10M rows, k <= 52k: 16), a sample
         // of runs of 4 16-row tiles, one in hstride: an estimated threshold (see K6h)
         int hstride = 1;
-        // (HCRAG_K6H_RATIO: sampled rows per k the next stride must leave, default 100; A/B)
-        const int64_t ratio = hooks().k6h_ratio ? hooks().k6h_ratio : 100;
+        // (the next stride must leave >= 12 k sampled rows; r06ah, deep k = 5000 on 1M x 384,
+        // alternating processes: 100 -- the r05 rule -- 0.675 ms, 25 0.64-0.68, 12 0.63 (a 1/16
+        // sample); at 10M rows the stride is 16 either way.  HCRAG_K6H_RATIO overrides, A/B)
+        const int64_t ratio = hooks().k6h_ratio ? hooks().k6h_ratio : 12;
         while (hstride < 16 && ix->n / (2 * hstride) >= ratio * k) hstride *= 2;
         const int64_t ntile16 = (ix->n + 15) / 16, run = 4 * (int64_t)hstride;
         const int64_t stiles = ntile16 / run * 4 + std::min<int64_t>(4, ntile16 % run);
