@@ -40,6 +40,10 @@ def main():
                 es, ei = O.cosine_topk(Q, R, k)
                 check(s, i, es, ei)
                 assert ix.last_stats()["fallback_queries"] == B
+            # two whole groups (no partial group)
+            s, i = ix.search(Q[:64], 3000)
+            es, ei = O.cosine_topk(Q[:64], R, 3000)
+            check(s, i, es, ei)
             mask = rng.random(N) < 0.6
             ix.set_rowmask(mask)
             s, i = ix.search(Q[:40], 2500)
