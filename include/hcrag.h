@@ -117,9 +117,10 @@ int hcr_search(hcr_index* index, const float* queries, int64_t nq, int k, int sc
 
 /* Device variant: queries (float32, nq x dim), outputs in device memory; fp64 scores so
  * that row-sharded results merge exactly across GPUs.  Kernels run on `stream` (NULL = the
- * legacy default stream); the call
- * synchronises that stream once per pass to read the certificate count, so
- * outputs are final when it returns. */
+ * legacy default stream); the call waits once per pass for the certificate count (DESIGN.md
+ * §4) -- by default for the pass's last launch to store it in pinned host memory, which it does
+ * after every write of the outputs (HCR_OPT_FLAG_READ) -- so outputs are final when it returns
+ * and later work on `stream` is ordered after them. */
 int hcr_search_device(hcr_index* index, const float* d_queries, int64_t nq, int k,
                       int score_mode, double threshold, double* d_out_scores,
                       int64_t* d_out_ids, void* stream);
